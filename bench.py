@@ -1,0 +1,218 @@
+"""Benchmark: CFG denoising steps/s (T=1000, 32x32x4 latents, B=64 per GPU) on MI355X.
+
+A "step" is one Diffuser.denoise_cond over the batch (reference diff.py:127-162):
+two U-Net forwards (uncond + cond, batched as one 2B = 128-sample native forward)
+plus the CFG mix and the DDPM update, with on-device Philox noise; the timed steps
+run as replayed hipGraphs (the diff.py:332-344 loop without host round trips).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N  (one rank per GPU)
+
+Each rank runs its own B=64 shard (weak scaling: samples are independent — no
+per-step collective); frozen weights are broadcast from rank 0 over RCCL once.
+`value` = batch-steps/s of the whole job = N * K / max-over-ranks time.
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.join(REPO, "diffusion-model_amd"), REPO):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X dense fp32 (MI355X_MICROARCH.md, chip table)
+HBM_PEAK_GBS = 8000.0
+UNET_GFLOP_PER_SAMPLE = 3.7097  # reference FLOPs per sample-forward
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--hw", type=int, default=32)
+    ap.add_argument("--T", type=int, default=1000)
+    ap.add_argument("--guidance", type=float, default=3.0)
+    ap.add_argument("--cpu-steps", type=int, default=3, help="oracle steps timed for cpu_baseline (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-profile", action="store_true")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def make_inputs(B, hw, dev, seed=0):
+    """Synthetic config-2 inputs: x_T ~ N(0,1), y cycles 1,2,3,
+    cond U[0,1) masked to the class keys of diff.py:235-239."""
+    from diff import CLASS_KEYS, KEY_ORDER
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn((B, 4, hw, hw), generator=g)
+    y = torch.tensor([1 + i % 3 for i in range(B)], dtype=torch.long)
+    mask = torch.zeros((B, 12))
+    for i in range(B):
+        for k in CLASS_KEYS[int(y[i])]:
+            mask[i, KEY_ORDER.index(k)] = 1.0
+    vals = torch.rand((B, 12), generator=g) * mask
+    return x.to(dev), y.to(dev), vals.to(dev), mask.to(dev)
+
+
+def cpu_baseline(args):
+    """The oracle (reference-equivalent torch-CPU restatement, bit-exact with the reference on this
+    container) timed on the host cores: a bounded sample of CFG steps at the benchmark shape."""
+    from dmx import synth
+    from oracle import ref
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    torch.set_num_threads(threads)
+    sd = synth.unet_cond_geom_weights(0)
+    x, y, vals, mask = make_inputs(args.batch, args.hw, "cpu")
+    _, a, ab = ref.schedule(args.T)
+    t = torch.full((args.batch,), args.T, dtype=torch.long)
+    with torch.no_grad():
+        ref.cfg_step(sd, x, t, y, a, ab, args.guidance, 0, vals, mask, torch.randn(x.shape))  # warm-up
+        t0 = time.perf_counter()
+        for _ in range(args.cpu_steps):
+            x = ref.cfg_step(sd, x, t, y, a, ab, args.guidance, 0, vals, mask, torch.randn(x.shape))
+        dt = time.perf_counter() - t0
+    return {"value": args.cpu_steps / dt, "unit": "CFG batch-steps/s (B=%d)" % args.batch, "cores": threads,
+            "kind": "port",
+            "sample": f"{args.cpu_steps} CFG steps at B={args.batch}, {args.hw}x{args.hw}x4, after 1 warm-up "
+                      f"(oracle/ref.py, torch-CPU fp32, {threads} threads)"}
+
+
+def roofline(records, pmc=None):
+    """Dominant kernel = the kernel name with the largest summed duration in one eager,
+    event-timed step; achieved = its algorithmic FLOPs / its event-timed duration."""
+    agg = {}
+    for r in records:
+        a = agg.setdefault(r["kernel"], {"ms": 0.0, "flops": 0.0, "bytes": 0.0, "n": 0})
+        a["ms"] += r["ms"]
+        a["flops"] += r["flops"]
+        a["bytes"] += r["bytes"]
+        a["n"] += 1
+    name, a = max(agg.items(), key=lambda kv: kv[1]["ms"])
+    avg_ms = a["ms"] / a["n"]
+    flops_per_launch = a["flops"] / a["n"]
+    achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
+    traffic = None
+    if pmc and name in pmc:
+        traffic = pmc[name]
+    total_ms = sum(v["ms"] for v in agg.values())
+    total_flops = sum(v["flops"] for v in agg.values())
+    return {"kernel": name, "bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
+            "launches": a["n"], "avg_launch_us": round(avg_ms * 1e3, 2),
+            "flops_per_launch": flops_per_launch,
+            "step_kernel_ms": round(total_ms, 3),
+            "step_tflops_eager": round(total_flops / (total_ms * 1e-3) / 1e12, 3)}, agg
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    import diff
+    from dmx import synth
+    from models.unet_cond_geom import UnetCondWithGeomHead
+
+    model = UnetCondWithGeomHead()
+    if rank == 0 or world == 1:
+        model.load_state_dict(synth.unet_cond_geom_weights(0))
+    model.to(dev).eval()
+    if world > 1:  # C1: broadcast the frozen weights once over RCCL (xGMI)
+        import torch.distributed as dist
+        for p in model.parameters():
+            dist.broadcast(p.data, src=0)
+    nm = model.native()
+    d = diff.Diffuser(args.T, device=dev)
+    tables = d.coef_tables(dev, True)
+    x, y, vals, mask = make_inputs(args.batch, args.hw, dev, seed=rank)
+    t_dev = torch.full((1,), args.T, dtype=torch.long, device=dev)
+    seed = 1234
+
+    # warm-up (also captures the step graph)
+    nm.sample_loop(x, t_dev, y, 0, vals, mask, args.guidance, tables, max(args.warmup, 1), seed=seed,
+                   sample_offset=rank * args.batch)
+    torch.cuda.synchronize()
+    t_dev.fill_(args.T)
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    nm.sample_loop(x, t_dev, y, 0, vals, mask, args.guidance, tables, args.steps, seed=seed,
+                   sample_offset=rank * args.batch)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    assert torch.isfinite(x).all(), "non-finite latents"
+
+    value = world * args.steps / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    out = {
+        "metric": "denoising steps/sec (CFG, T=1000, 32x32x4 latent, B=64)",
+        "value": round(value, 3),
+        "unit": "CFG batch-steps/s (B=64 per GPU; 2 U-Net forwards + update each)",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f32", "data": "synthetic (seeded synthetic weights, x_T~N(0,1), Philox step noise)",
+        "config": {"workload": "config 2: UnetCondWithGeomHead CFG=3.0 denoising step, B=64, 32x32x4, T=1000",
+                   "global_batch": args.batch * world, "latent": [4, args.hw, args.hw], "T": args.T,
+                   "parallelism": f"sample-sharded x{world} (no per-step collective)"},
+        "sample_steps_per_s": round(value * args.batch, 1),
+        "tflops_effective": round(value * 2 * args.batch * UNET_GFLOP_PER_SAMPLE / 1e3, 2),
+    }
+    if rank == 0:
+        if not args.no_profile:
+            xp = x.clone()
+            tp = torch.full((args.batch,), args.T, dtype=torch.long, device=dev)
+            nm.step_profile(xp, xp, tp, y, 0, vals, mask, args.guidance, tables, None, seed=seed)  # warm
+            recs = nm.step_profile(xp, xp, tp, y, 0, vals, mask, args.guidance, tables, None, seed=seed)
+            pmc = None
+            pmc_path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+            if os.path.exists(pmc_path):
+                pmc = json.load(open(pmc_path)).get("traffic_bytes_per_launch")
+            rl, agg = roofline(recs, pmc)
+            out["roofline"] = rl
+            if os.environ.get("DMX_BENCH_BREAKDOWN"):
+                with open(os.environ["DMX_BENCH_BREAKDOWN"], "w") as f:
+                    json.dump({"records": recs, "by_kernel": agg}, f, indent=1)
+        if args.cpu_steps > 0 and world == 1:
+            out["cpu_baseline"] = cpu_baseline(args)
+            out["gpu_over_cpu"] = round(value / out["cpu_baseline"]["value"], 1)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,1315 @@
+// dmx engine: weights, workspace planning, U-Net / VAE orchestration, hipGraph
+// step loop and the C ABI of include/dmx.h.
+#include "dmx.h"
+
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "igemm.h"
+#include "kernels.h"
+
+namespace dmx {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+static thread_local std::string g_err;
+
+#define HIPCHK(x)                                                                               \
+  do {                                                                                          \
+    hipError_t e_ = (x);                                                                        \
+    if (e_ != hipSuccess) throw Error(DMX_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+#define REQUIRE(c, msg)                                    \
+  do {                                                     \
+    if (!(c)) throw Error(DMX_E_ARG, std::string(msg));    \
+  } while (0)
+
+static inline int rup(int a, int b) { return (a + b - 1) / b * b; }
+static inline int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+// ===========================================================================
+// Reference state_dict key lists (mirror of dmx/spec.py; the checkpoint contract
+// of Utils.loadModel, utils.py:68-73).
+// ===========================================================================
+struct Key {
+  std::string name;
+  std::vector<int64_t> shape;
+};
+using Keys = std::vector<Key>;
+
+static void k_res(Keys& k, const std::string& p, int cin, int cout, int mid = 0) {
+  mid = mid ? mid : cout;
+  k.push_back({p + ".double_conv.0.weight", {mid, cin, 3, 3}});
+  k.push_back({p + ".double_conv.1.weight", {mid}});
+  k.push_back({p + ".double_conv.1.bias", {mid}});
+  k.push_back({p + ".double_conv.3.weight", {cout, mid, 3, 3}});
+  k.push_back({p + ".double_conv.4.weight", {cout}});
+  k.push_back({p + ".double_conv.4.bias", {cout}});
+}
+static void k_lin(Keys& k, const std::string& p, int fin, int fout) {
+  k.push_back({p + ".weight", {fout, fin}});
+  k.push_back({p + ".bias", {fout}});
+}
+static void k_attn(Keys& k, const std::string& p, int c) {
+  k.push_back({p + ".mha.in_proj_weight", {3 * c, c}});
+  k.push_back({p + ".mha.in_proj_bias", {3 * c}});
+  k.push_back({p + ".mha.out_proj.weight", {c, c}});
+  k.push_back({p + ".mha.out_proj.bias", {c}});
+  k.push_back({p + ".ln.weight", {c}});
+  k.push_back({p + ".ln.bias", {c}});
+  k.push_back({p + ".ff_self.0.weight", {c}});
+  k.push_back({p + ".ff_self.0.bias", {c}});
+  k_lin(k, p + ".ff_self.1", c, c);
+  k_lin(k, p + ".ff_self.3", c, c);
+}
+
+struct Topo {
+  char kind;  // r(es) d(own) u(p) a(ttn)
+  std::string name;
+  int a, b;
+};
+static std::vector<Topo> unet_topo(int in_ch, bool deep) {
+  std::vector<Topo> t = {{'r', "inc", in_ch, 64},   {'d', "down1", 64, 128}, {'a', "sa1", 128, 0},
+                         {'d', "down2", 128, 256}, {'a', "sa2", 256, 0},    {'d', "down3", 256, 256},
+                         {'a', "sa3", 256, 0}};
+  if (deep) {
+    t.push_back({'r', "bot1", 256, 512});
+    t.push_back({'r', "bot2", 512, 512});
+    t.push_back({'r', "bot3", 512, 256});
+  } else {
+    t.push_back({'r', "bot1", 256, 256});
+    t.push_back({'r', "bot3", 256, 256});
+  }
+  std::vector<Topo> rest = {{'u', "up1", 512, 128}, {'a', "sa4", 128, 0}, {'u', "up2", 256, 64},
+                            {'a', "sa5", 64, 0},    {'u', "up3", 128, 64}, {'a', "sa6", 64, 0}};
+  t.insert(t.end(), rest.begin(), rest.end());
+  return t;
+}
+
+static Keys model_keys(int kind, int in_ch, bool deep) {
+  Keys k;
+  if (kind == DMX_VAE) {
+    // models/vae.py:17-49
+    const int enc[][4] = {{0, 3, 64, 3},    {3, 64, 64, 4},    {6, 64, 128, 3},
+                          {9, 128, 128, 4}, {12, 128, 256, 3}, {15, 256, 256, 4}};
+    for (auto& e : enc) {
+      k.push_back({"enc." + std::to_string(e[0]) + ".weight", {e[2], e[1], e[3], e[3]}});
+      k.push_back({"enc." + std::to_string(e[0]) + ".bias", {e[2]}});
+      k.push_back({"enc." + std::to_string(e[0] + 1) + ".weight", {e[2]}});
+      k.push_back({"enc." + std::to_string(e[0] + 1) + ".bias", {e[2]}});
+    }
+    k.push_back({"to_mu.weight", {4, 256, 1, 1}});
+    k.push_back({"to_mu.bias", {4}});
+    k.push_back({"to_logvar.weight", {4, 256, 1, 1}});
+    k.push_back({"to_logvar.bias", {4}});
+    const int dec[][5] = {{0, 4, 256, 3, 0},    {3, 256, 256, 4, 1}, {6, 256, 128, 3, 0},
+                          {9, 128, 128, 4, 1},  {12, 128, 64, 3, 0}, {15, 64, 64, 4, 1}};
+    for (auto& d : dec) {
+      if (d[4]) k.push_back({"dec." + std::to_string(d[0]) + ".weight", {d[1], d[2], 4, 4}});
+      else k.push_back({"dec." + std::to_string(d[0]) + ".weight", {d[2], d[1], d[3], d[3]}});
+      k.push_back({"dec." + std::to_string(d[0]) + ".bias", {d[2]}});
+      k.push_back({"dec." + std::to_string(d[0] + 1) + ".weight", {d[2]}});
+      k.push_back({"dec." + std::to_string(d[0] + 1) + ".bias", {d[2]}});
+    }
+    k.push_back({"dec.18.weight", {3, 64, 3, 3}});
+    k.push_back({"dec.18.bias", {3}});
+    return k;
+  }
+  const bool cond = kind == DMX_UNET_COND_GEOM || kind == DMX_UNET_COND;
+  if (cond) {
+    k.push_back({"class_emb.weight", {4, 256}});
+    k_lin(k, "cond_mlp.0", 24, 256);
+    k_lin(k, "cond_mlp.2", 256, 256);
+  }
+  for (auto& t : unet_topo(in_ch, deep)) {
+    if (t.kind == 'r') k_res(k, t.name, t.a, t.b);
+    else if (t.kind == 'd') {
+      k_res(k, t.name + ".maxpool_conv.1", t.a, t.a);
+      k_res(k, t.name + ".maxpool_conv.2", t.a, t.b);
+      k_lin(k, t.name + ".emb_layer.1", 256, t.b);
+    } else if (t.kind == 'u') {
+      k_res(k, t.name + ".conv.0", t.a, t.a);
+      k_res(k, t.name + ".conv.1", t.a, t.b, t.a / 2);
+      k_lin(k, t.name + ".emb_layer.1", 256, t.b);
+    } else {
+      k_attn(k, t.name, t.a);
+    }
+  }
+  k.push_back({"out.weight", {in_ch, 64, 1, 1}});
+  k.push_back({"out.bias", {in_ch}});
+  if (kind == DMX_UNET_COND_GEOM) {
+    k_lin(k, "geom_head.mlp.0", 64, 256);
+    k_lin(k, "geom_head.mlp.2", 256, 12);
+  }
+  return k;
+}
+
+// ===========================================================================
+// Packed weights
+// ===========================================================================
+struct ConvW {
+  float* B = nullptr;
+  float* bias = nullptr;
+  int cin = 0, cout = 0, taps = 0, kpad = 0, npad = 0, phases = 1;
+};
+struct Vec {
+  float* p = nullptr;
+};
+struct ResW {
+  ConvW c1, c2;
+  Vec g1, b1, g2, b2;
+  int cin = 0, mid = 0, cout = 0;
+};
+struct AttnW {
+  ConvW qkv, o, f1, f2;
+  Vec l1w, l1b, l2w, l2b;
+  int c = 0;
+};
+struct DownUpW {
+  ResW r0, r1;
+  int emb_off = 0, cout = 0;
+};
+
+// Workspace: bump allocator run twice (plan: sizes only, then real).
+struct Arena {
+  char* base = nullptr;
+  size_t cap = 0, off = 0;
+  bool plan = true;
+  template <typename T>
+  T* get(size_t count) {
+    const size_t bytes = (count * sizeof(T) + 255) & ~(size_t)255;
+    char* p = base + off;
+    off += bytes;
+    return reinterpret_cast<T*>(plan ? nullptr : p);
+  }
+};
+
+struct GraphKey {
+  dmx_step_args a;
+  int steps_unused;
+  bool operator==(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(GraphKey)) == 0; }
+};
+
+}  // namespace dmx
+
+struct dmx_ctx {
+  int device = 0;
+  float* pos_table = nullptr;
+  int tmax = 0;
+};
+
+struct dmx_model {
+  dmx_ctx* ctx = nullptr;
+  int kind = 0, in_ch = 4;
+  bool deep = true;
+  bool finalized = false;
+  dmx::Keys keys;
+  std::map<std::string, std::pair<const float*, std::vector<int64_t>>> inputs;
+  std::vector<void*> owned;
+  // U-Net
+  dmx::ResW inc, bot[3];
+  int nbot = 0;
+  dmx::DownUpW down[3], up[3];
+  dmx::AttnW sa[6];
+  float *class_emb = nullptr, *w0 = nullptr, *b0 = nullptr, *w2t = nullptr, *b2 = nullptr, *wht = nullptr,
+        *bh = nullptr;
+  int hsum = 0;
+  float *out_w = nullptr, *out_b = nullptr, *gw0 = nullptr, *gb0 = nullptr, *gw2 = nullptr, *gb2 = nullptr;
+  // VAE decoder
+  dmx::ConvW vconv[4], vconvt[3];
+  dmx::Vec vg[6], vb[6];
+  // workspace + graph
+  dmx::Arena ws;
+  void* ws_mem = nullptr;
+  size_t ws_cap = 0;
+  hipGraphExec_t gexec = nullptr;
+  hipGraph_t graph = nullptr;
+  dmx::GraphKey gkey{};
+  bool has_graph = false;
+  // debug taps: (name, device pointer into the workspace, element count, C)
+  bool debug = false;
+  std::vector<std::pair<std::string, std::pair<const float*, size_t>>> taps;
+};
+
+namespace dmx {
+
+// ---------------------------------------------------------------------------
+// weight packing helpers (device-side repack of the caller's tensors)
+// ---------------------------------------------------------------------------
+struct Packer {
+  dmx_model* m;
+  hipStream_t st;
+  const std::pair<const float*, std::vector<int64_t>>& in(const std::string& name) {
+    auto it = m->inputs.find(name);
+    if (it == m->inputs.end()) throw Error(DMX_E_STATE, "missing weight tensor '" + name + "'");
+    return it->second;
+  }
+  float* alloc(size_t n) {
+    void* p = nullptr;
+    HIPCHK(hipMalloc(&p, n * sizeof(float) + 256));
+    m->owned.push_back(p);
+    return static_cast<float*>(p);
+  }
+  float* copy(const std::string& name) {
+    auto& t = in(name);
+    size_t n = 1;
+    for (auto s : t.second) n *= (size_t)s;
+    float* d = alloc(n);
+    HIPCHK(hipMemcpyAsync(d, t.first, n * sizeof(float), hipMemcpyDeviceToDevice, st));
+    return d;
+  }
+  Vec vec(const std::string& name) { return Vec{copy(name)}; }
+  void repack(float* dst, const float* src, int kind, int P, int npad, int kpad, int cout, int cin, int ks) {
+    const size_t total = (size_t)P * npad * kpad;
+    const int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
+    repack_kernel<<<blocks, 256, 0, st>>>(dst, src, kind, P, npad, kpad, cout, cin, ks);
+    HIPCHK(hipGetLastError());
+  }
+  // Conv2d [cout][cin][ks][ks]; channel-padded to cin_pad (in_ch=3 first layer)
+  ConvW conv(const std::string& w, const std::string& b, int cin, int cout, int ks, int cin_pad = 0) {
+    ConvW c;
+    cin_pad = cin_pad ? cin_pad : cin;
+    c.cin = cin_pad;
+    c.cout = cout;
+    c.taps = ks * ks;
+    c.kpad = rup(c.taps * cin_pad, IG_BK);
+    c.npad = rup(cout, 128);
+    c.B = alloc((size_t)c.npad * c.kpad);
+    if (cin_pad == cin) {
+      repack(c.B, in(w).first, 0, 1, c.npad, c.kpad, cout, cin, ks);
+    } else {
+      // pad input channels: repack into a temporary [cout][cin_pad][ks][ks] first
+      float* tmp = alloc((size_t)cout * cin_pad * ks * ks);
+      HIPCHK(hipMemsetAsync(tmp, 0, (size_t)cout * cin_pad * ks * ks * sizeof(float), st));
+      for (int o = 0; o < cout; ++o)
+        HIPCHK(hipMemcpyAsync(tmp + (size_t)o * cin_pad * ks * ks, in(w).first + (size_t)o * cin * ks * ks,
+                              (size_t)cin * ks * ks * sizeof(float), hipMemcpyDeviceToDevice, st));
+      repack(c.B, tmp, 0, 1, c.npad, c.kpad, cout, cin_pad, ks);
+    }
+    if (!b.empty()) c.bias = copy(b);
+    return c;
+  }
+  ConvW linear(const std::string& w, const std::string& b, int fin, int fout) {
+    ConvW c;
+    c.cin = fin;
+    c.cout = fout;
+    c.taps = 1;
+    c.kpad = rup(fin, IG_BK);
+    c.npad = rup(fout, 128);
+    c.B = alloc((size_t)c.npad * c.kpad);
+    repack(c.B, in(w).first, 1, 1, c.npad, c.kpad, fout, fin, 1);
+    c.bias = copy(b);
+    return c;
+  }
+  ConvW convt(const std::string& w, const std::string& b, int cin, int cout) {
+    ConvW c;
+    c.cin = cin;
+    c.cout = cout;
+    c.taps = 4;
+    c.phases = 4;
+    c.kpad = rup(4 * cin, IG_BK);
+    c.npad = rup(cout, 128);
+    c.B = alloc((size_t)4 * c.npad * c.kpad);
+    repack(c.B, in(w).first, 2, 4, c.npad, c.kpad, cout, cin, 4);
+    c.bias = copy(b);
+    return c;
+  }
+  ResW res(const std::string& p, int cin, int cout, int mid = 0, int cin_pad = 0) {
+    ResW r;
+    mid = mid ? mid : cout;
+    r.cin = cin_pad ? cin_pad : cin;
+    r.mid = mid;
+    r.cout = cout;
+    r.c1 = conv(p + ".double_conv.0.weight", "", cin, mid, 3, cin_pad);
+    r.g1 = vec(p + ".double_conv.1.weight");
+    r.b1 = vec(p + ".double_conv.1.bias");
+    r.c2 = conv(p + ".double_conv.3.weight", "", mid, cout, 3);
+    r.g2 = vec(p + ".double_conv.4.weight");
+    r.b2 = vec(p + ".double_conv.4.bias");
+    return r;
+  }
+  AttnW attn(const std::string& p, int c) {
+    AttnW a;
+    a.c = c;
+    a.qkv = linear(p + ".mha.in_proj_weight", p + ".mha.in_proj_bias", c, 3 * c);
+    a.o = linear(p + ".mha.out_proj.weight", p + ".mha.out_proj.bias", c, c);
+    a.l1w = vec(p + ".ln.weight");
+    a.l1b = vec(p + ".ln.bias");
+    a.l2w = vec(p + ".ff_self.0.weight");
+    a.l2b = vec(p + ".ff_self.0.bias");
+    a.f1 = linear(p + ".ff_self.1.weight", p + ".ff_self.1.bias", c, c);
+    a.f2 = linear(p + ".ff_self.3.weight", p + ".ff_self.3.bias", c, c);
+    return a;
+  }
+  float* transposed(const std::string& name, int rows, int cols) {
+    float* d = alloc((size_t)rows * cols);
+    transpose_kernel<<<std::min(cdiv(rows * cols, 256), 4096), 256, 0, st>>>(d, in(name).first, rows, cols);
+    HIPCHK(hipGetLastError());
+    return d;
+  }
+};
+
+static void finalize_model(dmx_model* m, hipStream_t st) {
+  for (auto& k : m->keys) {
+    auto it = m->inputs.find(k.name);
+    if (it == m->inputs.end()) throw Error(DMX_E_STATE, "missing weight tensor '" + k.name + "'");
+    if (it->second.second != k.shape) throw Error(DMX_E_ARG, "shape mismatch for '" + k.name + "'");
+  }
+  Packer P{m, st};
+  if (m->kind == DMX_VAE) {
+    m->vconv[0] = P.conv("dec.0.weight", "dec.0.bias", 4, 256, 3);
+    m->vconvt[0] = P.convt("dec.3.weight", "dec.3.bias", 256, 256);
+    m->vconv[1] = P.conv("dec.6.weight", "dec.6.bias", 256, 128, 3);
+    m->vconvt[1] = P.convt("dec.9.weight", "dec.9.bias", 128, 128);
+    m->vconv[2] = P.conv("dec.12.weight", "dec.12.bias", 128, 64, 3);
+    m->vconvt[2] = P.convt("dec.15.weight", "dec.15.bias", 64, 64);
+    const int gi[6] = {1, 4, 7, 10, 13, 16};
+    for (int i = 0; i < 6; ++i) {
+      m->vg[i] = P.vec("dec." + std::to_string(gi[i]) + ".weight");
+      m->vb[i] = P.vec("dec." + std::to_string(gi[i]) + ".bias");
+    }
+    m->vconv[3].B = P.copy("dec.18.weight");
+    m->vconv[3].bias = P.copy("dec.18.bias");
+  } else {
+    const bool cond = m->kind != DMX_UNET;
+    const int cin_pad = rup(m->in_ch, 4);
+    m->inc = P.res("inc", m->in_ch, 64, 0, cin_pad);
+    const char* dn[3] = {"down1", "down2", "down3"};
+    const int dci[3] = {64, 128, 256}, dco[3] = {128, 256, 256};
+    const char* un[3] = {"up1", "up2", "up3"};
+    const int uci[3] = {512, 256, 128}, uco[3] = {128, 64, 64};
+    int off = 0;
+    for (int i = 0; i < 3; ++i) {
+      m->down[i].r0 = P.res(std::string(dn[i]) + ".maxpool_conv.1", dci[i], dci[i]);
+      m->down[i].r1 = P.res(std::string(dn[i]) + ".maxpool_conv.2", dci[i], dco[i]);
+      m->down[i].emb_off = off;
+      m->down[i].cout = dco[i];
+      off += dco[i];
+    }
+    for (int i = 0; i < 3; ++i) {
+      m->up[i].r0 = P.res(std::string(un[i]) + ".conv.0", uci[i], uci[i]);
+      m->up[i].r1 = P.res(std::string(un[i]) + ".conv.1", uci[i], uco[i], uci[i] / 2);
+      m->up[i].emb_off = off;
+      m->up[i].cout = uco[i];
+      off += uco[i];
+    }
+    m->hsum = off;
+    if (m->deep) {
+      m->bot[0] = P.res("bot1", 256, 512);
+      m->bot[1] = P.res("bot2", 512, 512);
+      m->bot[2] = P.res("bot3", 512, 256);
+      m->nbot = 3;
+    } else {
+      m->bot[0] = P.res("bot1", 256, 256);
+      m->bot[1] = P.res("bot3", 256, 256);
+      m->nbot = 2;
+    }
+    const int sac[6] = {128, 256, 256, 128, 64, 64};
+    for (int i = 0; i < 6; ++i) m->sa[i] = P.attn("sa" + std::to_string(i + 1), sac[i]);
+    // embedding heads: transposed & concatenated [256][hsum]
+    m->wht = P.alloc((size_t)256 * m->hsum);
+    m->bh = P.alloc(m->hsum);
+    const char* all[6] = {"down1", "down2", "down3", "up1", "up2", "up3"};
+    const int hc[6] = {128, 256, 256, 128, 64, 64};
+    int o = 0;
+    for (int i = 0; i < 6; ++i) {
+      float* tp = P.transposed(std::string(all[i]) + ".emb_layer.1.weight", hc[i], 256);  // [256][hc]
+      for (int r = 0; r < 256; ++r)
+        HIPCHK(hipMemcpyAsync(m->wht + (size_t)r * m->hsum + o, tp + (size_t)r * hc[i], hc[i] * sizeof(float),
+                              hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipMemcpyAsync(m->bh + o, P.in(std::string(all[i]) + ".emb_layer.1.bias").first,
+                            hc[i] * sizeof(float), hipMemcpyDeviceToDevice, st));
+      o += hc[i];
+    }
+    if (cond) {
+      m->class_emb = P.copy("class_emb.weight");
+      m->w0 = P.copy("cond_mlp.0.weight");
+      m->b0 = P.copy("cond_mlp.0.bias");
+      m->w2t = P.transposed("cond_mlp.2.weight", 256, 256);
+      m->b2 = P.copy("cond_mlp.2.bias");
+    }
+    m->out_w = P.copy("out.weight");
+    m->out_b = P.copy("out.bias");
+    if (m->kind == DMX_UNET_COND_GEOM) {
+      m->gw0 = P.copy("geom_head.mlp.0.weight");
+      m->gb0 = P.copy("geom_head.mlp.0.bias");
+      m->gw2 = P.copy("geom_head.mlp.2.weight");
+      m->gb2 = P.copy("geom_head.mlp.2.bias");
+    }
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  m->inputs.clear();  // caller's tensors are no longer referenced
+  m->finalized = true;
+}
+
+// ===========================================================================
+// Launch helpers
+// ===========================================================================
+struct ProfRec {
+  std::string kernel, layer;
+  double flops, bytes;
+  hipEvent_t e0, e1;
+};
+struct Prof {
+  std::vector<ProfRec> recs;
+  std::vector<hipEvent_t> pool;
+  hipEvent_t ev() {
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    pool.push_back(e);
+    return e;
+  }
+  ~Prof() {
+    for (auto e : pool) (void)hipEventDestroy(e);
+  }
+};
+
+struct Run {
+  dmx_model* m;
+  hipStream_t st;
+  bool plan;
+  Arena& ws;
+  Prof* prof = nullptr;
+  std::string layer;
+  void tap(const std::string& name, const float* p, size_t count);
+  void begin(const std::string& kernel, double flops, double bytes) {
+    if (!prof) return;
+    ProfRec r{kernel, layer, flops, bytes, prof->ev(), prof->ev()};
+    HIPCHK(hipEventRecord(r.e0, st));
+    prof->recs.push_back(r);
+  }
+  void end() {
+    if (!prof) return;
+    HIPCHK(hipEventRecord(prof->recs.back().e1, st));
+  }
+};
+
+void Run::tap(const std::string& name, const float* p, size_t count) {
+  if (plan || !m->debug) return;
+  m->taps.push_back({name, {p, count}});
+}
+
+template <int BM, int BN, int SRC, int EPI>
+static void launch_ig(const IgemmParams& p, dim3 grid, hipStream_t st) {
+  igemm_f32_kernel<BM, BN, SRC, EPI><<<grid, 256, 0, st>>>(p);
+}
+
+template <int SRC, int EPI>
+static void launch_ig_tiles(int bm, int bn, const IgemmParams& p, dim3 grid, hipStream_t st) {
+  if (bm == 128 && bn == 128) launch_ig<128, 128, SRC, EPI>(p, grid, st);
+  else if (bm == 128) launch_ig<128, 64, SRC, EPI>(p, grid, st);
+  else if (bn == 128) launch_ig<64, 128, SRC, EPI>(p, grid, st);
+  else launch_ig<64, 64, SRC, EPI>(p, grid, st);
+}
+
+// Implicit GEMM: conv3x3 (taps 9), ConvT phases (taps 4, phases 4), linear (taps 1)
+static void gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, const ConvW& cw, int epi, float* out,
+                 const float* res, float2* rowpart, int seg) {
+  if (R.plan) return;
+  IgemmParams p;
+  std::memset(&p, 0, sizeof(p));
+  p.src = s;
+  p.H = H;
+  p.W = W;
+  p.M = N * H * W;
+  p.taps = cw.taps;
+  for (int ph = 0; ph < cw.phases; ++ph) {
+    for (int t = 0; t < cw.taps; ++t) {
+      if (cw.phases == 4) {
+        const int py = ph >> 1, px = ph & 1, jy = t >> 1, jx = t & 1;
+        p.dy[ph][t] = (int8_t)(py == 0 ? (jy == 0 ? 0 : -1) : (jy == 0 ? 1 : 0));
+        p.dx[ph][t] = (int8_t)(px == 0 ? (jx == 0 ? 0 : -1) : (jx == 0 ? 1 : 0));
+      } else if (cw.taps == 9) {
+        p.dy[ph][t] = (int8_t)(t / 3 - 1);
+        p.dx[ph][t] = (int8_t)(t % 3 - 1);
+      }
+    }
+    p.py[ph] = (int8_t)(cw.phases == 4 ? ph >> 1 : 0);
+    p.px[ph] = (int8_t)(cw.phases == 4 ? ph & 1 : 0);
+  }
+  p.Kreal = cw.taps * cw.cin;
+  p.Kpad = cw.kpad;
+  p.Cout = cw.cout;
+  p.Npad = cw.npad;
+  p.osy = p.osx = cw.phases == 4 ? 2 : 1;
+  p.Hout = H * p.osy;
+  p.Wout = W * p.osx;
+  p.Bw = cw.B;
+  p.bias = cw.bias;
+  p.out = out;
+  p.res = res;
+  p.rowpart = rowpart;
+  p.seg = seg;
+  if (s.C != cw.cin) throw Error(DMX_E_INTERNAL, "gemm: source channels != weight channels");
+  if (cw.cout % 32 != 0) throw Error(DMX_E_INTERNAL, "gemm: Cout must be a multiple of 32");
+  const int bn = (cw.cout % 128 == 0) ? 128 : 64;
+  const int tiles128 = cdiv(p.M, 128) * cdiv(cw.cout, bn) * cw.phases;
+  const int bm = tiles128 >= 512 ? 128 : 64;
+  dim3 grid(cdiv(p.M, bm), cdiv(cw.cout, bn), cw.phases);
+  {
+    const int creal = (src_mode == SRC_NCHW && s.C0) ? s.C0 : cw.cin;
+    const double flops = 2.0 * (double)p.M * cw.phases * cw.cout * (double)cw.taps * creal;
+    const double bytes = 4.0 * ((double)p.M * cw.phases * cw.cout + (double)p.M * s.C +
+                                (double)cw.phases * cw.cout * cw.taps * cw.cin);
+    char nm[96];
+    std::snprintf(nm, sizeof nm, "igemm_f32_kernel<%d, %d, %d, %d>", bm, bn, epi == EPI_STATS ? src_mode : SRC_PLAIN,
+                  epi);
+    R.begin(nm, flops, bytes);
+  }
+  switch (epi) {
+    case EPI_STATS:
+      switch (src_mode) {
+        case SRC_PLAIN: launch_ig_tiles<SRC_PLAIN, EPI_STATS>(bm, bn, p, grid, R.st); break;
+        case SRC_GNACT: launch_ig_tiles<SRC_GNACT, EPI_STATS>(bm, bn, p, grid, R.st); break;
+        case SRC_MAXPOOL: launch_ig_tiles<SRC_MAXPOOL, EPI_STATS>(bm, bn, p, grid, R.st); break;
+        case SRC_UPCAT: launch_ig_tiles<SRC_UPCAT, EPI_STATS>(bm, bn, p, grid, R.st); break;
+        case SRC_NCHW: launch_ig_tiles<SRC_NCHW, EPI_STATS>(bm, bn, p, grid, R.st); break;
+        default: throw Error(DMX_E_INTERNAL, "bad src mode");
+      }
+      break;
+    case EPI_BIAS: launch_ig_tiles<SRC_PLAIN, EPI_BIAS>(bm, bn, p, grid, R.st); break;
+    case EPI_BIAS_GELU: launch_ig_tiles<SRC_PLAIN, EPI_BIAS_GELU>(bm, bn, p, grid, R.st); break;
+    case EPI_BIAS_RES: launch_ig_tiles<SRC_PLAIN, EPI_BIAS_RES>(bm, bn, p, grid, R.st); break;
+    default: throw Error(DMX_E_INTERNAL, "bad epilogue");
+  }
+  R.end();
+  HIPCHK(hipGetLastError());
+}
+
+static void gn_finalize(Run& R, const float2* rowpart, float2* stats, int N, int HW, int nseg, int G, int C) {
+  if (R.plan) return;
+  R.begin("gn_finalize_kernel", 0.0, 8.0 * (double)N * HW * nseg);
+  gn_finalize_kernel<<<N * G, 256, 0, R.st>>>(rowpart, stats, HW, nseg, G, C, 1e-5f);
+  R.end();
+  HIPCHK(hipGetLastError());
+}
+
+static void finish(Run& R, const FinishParams& fp, int rmode) {
+  if (R.plan) return;
+  const size_t total = (size_t)fp.N * fp.H * fp.W * (fp.C / 4);
+  const int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
+  {
+    char nm[64];
+    std::snprintf(nm, sizeof nm, "finish_kernel<%d>", fp.has_res ? rmode : SRC_PLAIN);
+    R.begin(nm, 0.0, 4.0 * (double)total * 4 * (fp.has_res ? 3 : 2));
+  }
+  switch (rmode) {
+    case SRC_MAXPOOL: finish_kernel<SRC_MAXPOOL><<<blocks, 256, 0, R.st>>>(fp); break;
+    case SRC_UPCAT: finish_kernel<SRC_UPCAT><<<blocks, 256, 0, R.st>>>(fp); break;
+    case SRC_GNACT: finish_kernel<SRC_GNACT><<<blocks, 256, 0, R.st>>>(fp); break;
+    case SRC_NCHW: finish_kernel<SRC_NCHW><<<blocks, 256, 0, R.st>>>(fp); break;
+    default: finish_kernel<SRC_PLAIN><<<blocks, 256, 0, R.st>>>(fp); break;
+  }
+  R.end();
+  HIPCHK(hipGetLastError());
+}
+
+static SrcDesc plain_src(const float* p, int C) {
+  SrcDesc s;
+  std::memset(&s, 0, sizeof(s));
+  s.src0 = p;
+  s.C = C;
+  s.G = 1;
+  s.scale = 1.f;
+  return s;
+}
+
+// ResBlock (models/unet_cond.py:10-30): conv -> GN -> GELU -> conv -> GN [-> GELU(x + .)] [+ emb]
+static float* resblock(Run& R, const ResW& w, const SrcDesc& in, int mode, int N, int H, int W, bool residual,
+                       const float* emb, int emb_stride, int emb_off) {
+  const int M = N * H * W;
+  const int seg = 32;
+  float* r1 = R.ws.get<float>((size_t)M * w.mid);
+  float2* rp1 = R.ws.get<float2>((size_t)M * (w.mid / seg));
+  float2* st1 = R.ws.get<float2>(N);
+  gemm(R, in, mode, N, H, W, w.c1, EPI_STATS, r1, nullptr, rp1, seg);
+  gn_finalize(R, rp1, st1, N, H * W, w.mid / seg, 1, w.mid);
+  SrcDesc s2 = plain_src(r1, w.mid);
+  s2.stats = st1;
+  s2.gamma = w.g1.p;
+  s2.beta = w.b1.p;
+  s2.act = 1;
+  float* r2 = R.ws.get<float>((size_t)M * w.cout);
+  float2* rp2 = R.ws.get<float2>((size_t)M * (w.cout / seg));
+  float2* st2 = R.ws.get<float2>(N);
+  gemm(R, s2, SRC_GNACT, N, H, W, w.c2, EPI_STATS, r2, nullptr, rp2, seg);
+  gn_finalize(R, rp2, st2, N, H * W, w.cout / seg, 1, w.cout);
+  float* out = R.ws.get<float>((size_t)M * w.cout);
+  FinishParams fp;
+  std::memset(&fp, 0, sizeof(fp));
+  fp.raw = r2;
+  fp.stats = st2;
+  fp.gamma = w.g2.p;
+  fp.beta = w.b2.p;
+  fp.G = 1;
+  fp.C = w.cout;
+  fp.H = H;
+  fp.W = W;
+  fp.N = N;
+  fp.res = in;
+  fp.has_res = residual ? 1 : 0;
+  fp.emb = emb;
+  fp.emb_stride = emb_stride;
+  fp.emb_off = emb_off;
+  fp.out = out;
+  finish(R, fp, residual ? mode : SRC_PLAIN);
+  R.tap(R.layer + ".r1", r1, (size_t)M * w.mid);
+  R.tap(R.layer, out, (size_t)M * w.cout);
+  return out;
+}
+
+static void layernorm(Run& R, const float* x, float* y, const Vec& w, const Vec& b, int M, int C) {
+  if (R.plan) return;
+  const int blocks = cdiv(M, 4);
+  R.begin("layernorm_kernel<" + std::to_string(C / 64) + ">", 0.0, 8.0 * (double)M * C);
+  switch (C) {
+    case 64: layernorm_kernel<1><<<blocks, 256, 0, R.st>>>(x, y, w.p, b.p, M, 1e-5f); break;
+    case 128: layernorm_kernel<2><<<blocks, 256, 0, R.st>>>(x, y, w.p, b.p, M, 1e-5f); break;
+    case 256: layernorm_kernel<4><<<blocks, 256, 0, R.st>>>(x, y, w.p, b.p, M, 1e-5f); break;
+    default: throw Error(DMX_E_INTERNAL, "layernorm: unsupported C");
+  }
+  R.end();
+  HIPCHK(hipGetLastError());
+}
+
+static void attention_core(Run& R, const float* qkv, float* out, int N, int L, int C) {
+  if (R.plan) return;
+  const int D = C / 4;
+  const int qt = L >= 256 ? 2 : 1;
+  dim3 grid(cdiv(L, 64 * qt), 4, N);
+  R.begin("attention_kernel<" + std::to_string(D) + ", " + std::to_string(qt) + ">", 4.0 * N * (double)L * L * C,
+          4.0 * (double)N * L * 4 * C);
+#define ATT(DD, QQ) attention_kernel<DD, QQ><<<grid, 256, 0, R.st>>>(qkv, out, L, C)
+  if (D == 16) { if (qt == 2) ATT(16, 2); else ATT(16, 1); }
+  else if (D == 32) { if (qt == 2) ATT(32, 2); else ATT(32, 1); }
+  else if (D == 64) { if (qt == 2) ATT(64, 2); else ATT(64, 1); }
+  else throw Error(DMX_E_INTERNAL, "attention: unsupported head dim");
+#undef ATT
+  R.end();
+  HIPCHK(hipGetLastError());
+}
+
+// AttenionBlock (models/unet_cond.py:32-52) on NHWC == (N, L, C) tokens.
+static float* attn_block(Run& R, const AttnW& a, const float* x, int N, int H, int W) {
+  const int C = a.c, M = N * H * W, L = H * W;
+  float* xl = R.ws.get<float>((size_t)M * C);
+  float* qkv = R.ws.get<float>((size_t)M * 3 * C);
+  float* ao = R.ws.get<float>((size_t)M * C);
+  float* av = R.ws.get<float>((size_t)M * C);
+  float* al = R.ws.get<float>((size_t)M * C);
+  float* f = R.ws.get<float>((size_t)M * C);
+  float* out = R.ws.get<float>((size_t)M * C);
+  layernorm(R, x, xl, a.l1w, a.l1b, M, C);
+  gemm(R, plain_src(xl, C), SRC_PLAIN, N, H, W, a.qkv, EPI_BIAS, qkv, nullptr, nullptr, 1);
+  attention_core(R, qkv, ao, N, L, C);
+  gemm(R, plain_src(ao, C), SRC_PLAIN, N, H, W, a.o, EPI_BIAS_RES, av, xl, nullptr, 1);
+  layernorm(R, av, al, a.l2w, a.l2b, M, C);
+  gemm(R, plain_src(al, C), SRC_PLAIN, N, H, W, a.f1, EPI_BIAS_GELU, f, nullptr, nullptr, 1);
+  gemm(R, plain_src(f, C), SRC_PLAIN, N, H, W, a.f2, EPI_BIAS_RES, out, av, nullptr, 1);
+  R.tap(R.layer + ".xl", xl, (size_t)M * C);
+  R.tap(R.layer + ".qkv", qkv, (size_t)M * 3 * C);
+  R.tap(R.layer + ".ao", ao, (size_t)M * C);
+  R.tap(R.layer + ".av", av, (size_t)M * C);
+  R.tap(R.layer, out, (size_t)M * C);
+  return out;
+}
+
+struct FwdIn {
+  const float* x;        // NCHW (n_x samples)
+  int n_x;               // samples in x (N or N/2 under CFG batching)
+  const int64_t* t; int t_stride;
+  const int64_t* y; int y_null_first; int64_t y_null;
+  const float* vals; const float* mask; int cond_rows;
+};
+
+// UnetCond trunk (models/unet_cond_geom.py:52-76): returns the (N,H,W,64) feature
+static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
+  dmx_model* m = R.m;
+  // embedding
+  float* emb = R.ws.get<float>((size_t)N * m->hsum);
+  if (!R.plan) {
+    EmbedParams e;
+    std::memset(&e, 0, sizeof(e));
+    e.t = in.t;
+    e.t_stride = in.t_stride;
+    e.t_mod = in.n_x < N ? in.n_x : 0;
+    e.tmax = m->ctx->tmax;
+    e.y = m->kind == DMX_UNET ? nullptr : in.y;
+    e.y_null_first = in.y_null_first;
+    e.y_null = in.y_null;
+    e.n_half = in.y_null_first ? N / 2 : N;
+    e.vals = m->kind == DMX_UNET ? nullptr : in.vals;
+    e.mask = in.mask;
+    e.cond_rows = in.cond_rows > 0 ? in.cond_rows : N;
+    e.pos_table = m->ctx->pos_table;
+    e.class_emb = m->class_emb;
+    e.ncls = 4;
+    e.w0 = m->w0;
+    e.b0 = m->b0;
+    e.w2t = m->w2t;
+    e.b2 = m->b2;
+    e.wht = m->wht;
+    e.bh = m->bh;
+    e.hsum = m->hsum;
+    e.out = emb;
+    R.layer = "embed";
+    R.begin("embed_kernel", 2.0 * N * (24.0 * 256 + 256.0 * 256 + 256.0 * m->hsum), 4.0 * (256.0 * 256 + 256.0 * m->hsum));
+    embed_kernel<<<N, 256, 0, R.st>>>(e);
+    R.end();
+    R.tap("emb", emb, (size_t)N * m->hsum);
+    HIPCHK(hipGetLastError());
+  }
+  // inc
+  SrcDesc xs = plain_src(in.x, m->inc.cin);
+  xs.C0 = m->in_ch;
+  xs.n_mod = in.n_x < N ? in.n_x : 0;
+  R.layer = "inc";
+  float* x1 = resblock(R, m->inc, xs, SRC_NCHW, N, H, W, false, nullptr, 0, 0);
+  // down path: skips x1 (H), a1 (H/2), a2 (H/4)
+  const float* skips[3];
+  int sh[3], sw[3], sc[3];
+  const float* cur = x1;
+  int ch = H, cw = W, cc = 64;
+  for (int i = 0; i < 3; ++i) {
+    skips[i] = cur;
+    sh[i] = ch;
+    sw[i] = cw;
+    sc[i] = cc;
+    SrcDesc mp = plain_src(cur, cc);
+    mp.Hs = ch;
+    mp.Ws = cw;
+    const int nh = ch / 2, nw = cw / 2;
+    R.layer = "down" + std::to_string(i + 1) + ".0";
+    float* h0 = resblock(R, m->down[i].r0, mp, SRC_MAXPOOL, N, nh, nw, true, nullptr, 0, 0);
+    R.layer = "down" + std::to_string(i + 1) + ".1";
+    float* h1 = resblock(R, m->down[i].r1, plain_src(h0, cc), SRC_PLAIN, N, nh, nw, false, emb, m->hsum,
+                         m->down[i].emb_off);
+    cc = m->down[i].cout;
+    ch = nh;
+    cw = nw;
+    R.layer = "sa" + std::to_string(i + 1);
+    cur = attn_block(R, m->sa[i], h1, N, ch, cw);
+  }
+  // bottleneck
+  for (int i = 0; i < m->nbot; ++i) {
+    R.layer = "bot" + std::to_string(i + 1);
+    cur = resblock(R, m->bot[i], plain_src(cur, cc), SRC_PLAIN, N, ch, cw, false, nullptr, 0, 0);
+    cc = m->bot[i].cout;
+  }
+  // up path
+  for (int i = 0; i < 3; ++i) {
+    const int si = 2 - i;  // skip x3, x2, x1
+    SrcDesc u = plain_src(skips[si], sc[si] + cc);
+    u.C0 = sc[si];
+    u.src1 = cur;
+    u.Hs = ch;
+    u.Ws = cw;
+    const int dy = sh[si] - 2 * ch, dx = sw[si] - 2 * cw;
+    u.padT = dy > 0 ? dy / 2 : 0;
+    u.padL = dx > 0 ? dx / 2 : 0;
+    REQUIRE(u.C == m->up[i].r0.cin, "up: channel mismatch");
+    R.layer = "up" + std::to_string(i + 1) + ".0";
+    float* h0 = resblock(R, m->up[i].r0, u, SRC_UPCAT, N, sh[si], sw[si], true, nullptr, 0, 0);
+    R.layer = "up" + std::to_string(i + 1) + ".1";
+    float* h1 = resblock(R, m->up[i].r1, plain_src(h0, u.C), SRC_PLAIN, N, sh[si], sw[si], false, emb, m->hsum,
+                         m->up[i].emb_off);
+    ch = sh[si];
+    cw = sw[si];
+    cc = m->up[i].cout;
+    R.layer = "sa" + std::to_string(4 + i);
+    cur = attn_block(R, m->sa[3 + i], h1, N, ch, cw);
+  }
+  return const_cast<float*>(cur);
+}
+
+static void check_shapes(dmx_model* m, int n, int h, int w) {
+  if (!m->finalized) throw Error(DMX_E_STATE, "model weights not finalized");
+  if (m->kind == DMX_VAE) throw Error(DMX_E_ARG, "not a U-Net model");
+  REQUIRE(n >= 1, "batch must be >= 1");
+  REQUIRE(h >= 8 && w >= 8, "latent must be at least 8x8");
+  REQUIRE(h == w, "AttenionBlock assumes square maps (models/unet_cond.py:46-47)");
+  REQUIRE(m->ctx->pos_table != nullptr, "time table not set (dmx_set_time_table)");
+}
+
+static void ensure_ws(dmx_model* m) {
+  if (m->ws.off > m->ws_cap) {
+    if (m->ws_mem) HIPCHK(hipFree(m->ws_mem));
+    m->ws_mem = nullptr;
+    m->ws_cap = 0;
+    if (m->has_graph) {
+      (void)hipGraphExecDestroy(m->gexec);
+      (void)hipGraphDestroy(m->graph);
+      m->has_graph = false;
+    }
+    HIPCHK(hipMalloc(&m->ws_mem, m->ws.off));
+    m->ws_cap = m->ws.off;
+  }
+}
+
+template <typename F>
+static void run_planned(dmx_model* m, hipStream_t st, F&& body) {
+  m->ws.base = nullptr;
+  m->ws.off = 0;
+  m->ws.plan = true;
+  {
+    Run R{m, st, true, m->ws};
+    body(R);
+  }
+  ensure_ws(m);
+  m->ws.base = static_cast<char*>(m->ws_mem);
+  m->ws.off = 0;
+  m->ws.plan = false;
+  Run R{m, st, false, m->ws};
+  body(R);
+}
+
+static void step_body(Run& R, const dmx_step_args& a) {
+  dmx_model* m = R.m;
+  const bool cfg = m->kind != DMX_UNET && a.guidance > 0.f && a.y != nullptr;
+  const int N = cfg ? 2 * a.n : a.n;
+  FwdIn in{a.x_in, a.n, a.t, a.t_stride, a.y, cfg ? 1 : 0, a.null_label, a.vals, a.mask, a.n};
+  float* feat = unet_trunk(R, in, N, a.h, a.w);
+  if (R.plan) return;
+  StepTailParams p;
+  std::memset(&p, 0, sizeof(p));
+  p.feat = feat;
+  p.w = m->out_w;
+  p.b = m->out_b;
+  p.Co = m->in_ch;
+  p.B = a.n;
+  p.HW = a.h * a.w;
+  p.cfg = cfg ? 1 : 0;
+  p.guidance = a.guidance;
+  p.x = a.x_in;
+  p.x_out = a.x_out;
+  p.t = a.t;
+  p.t_stride = a.t_stride;
+  p.tmax = a.T;
+  p.c1 = a.c1;
+  p.c2 = a.c2;
+  p.sd = a.sd;
+  p.noise = a.noise;
+  p.seed = a.seed;
+  p.sample_offset = a.sample_offset;
+  dim3 grid(cdiv(p.HW, 256), a.n);
+  R.layer = "out+cfg+ddpm";
+  R.begin("step_tail_kernel", 2.0 * N * p.HW * 64.0 * p.Co, 4.0 * ((double)N * p.HW * 64 + 3.0 * a.n * p.HW * p.Co));
+  step_tail_kernel<<<grid, 256, 0, R.st>>>(p);
+  R.end();
+  HIPCHK(hipGetLastError());
+}
+
+static void validate_step(dmx_model* m, const dmx_step_args* a) {
+  REQUIRE(a != nullptr, "null step args");
+  check_shapes(m, a->n, a->h, a->w);
+  REQUIRE(a->x_in && a->x_out && a->t && a->c1 && a->c2 && a->sd, "null tensor in step args");
+  REQUIRE(a->T >= 1, "T must be >= 1");
+  REQUIRE(m->in_ch <= 4, "in_ch must be <= 4");
+  if (m->kind != DMX_UNET && a->guidance > 0.f) REQUIRE(a->y != nullptr, "CFG needs y");
+  if (m->kind == DMX_UNET_COND_GEOM || m->kind == DMX_UNET_COND)
+    REQUIRE((a->vals == nullptr) == (a->mask == nullptr), "vals and mask must be given together");
+}
+
+// VAE decoder (models/vae.py:35-49,64-69) on one chunk of n latents.
+static void vae_body(Run& R, const float* z, float* img, uint8_t* u8, int n, int h, int w) {
+  dmx_model* m = R.m;
+  const int G = 8;
+  SrcDesc s = plain_src(z, 4);
+  s.C0 = 4;
+  s.scale = 0.18215f;
+  int mode = SRC_NCHW;
+  int H = h, W = w;
+  const float* raw = nullptr;
+  const float2* stats = nullptr;
+  int C = 4;
+  for (int stage = 0; stage < 6; ++stage) {
+    const bool convt = stage & 1;
+    const ConvW& cw = convt ? m->vconvt[stage / 2] : m->vconv[stage / 2];
+    const int Ho = convt ? 2 * H : H, Wo = convt ? 2 * W : W;
+    const int Mo = n * Ho * Wo;
+    const int seg = std::min(32, cw.cout / G);
+    float* r = R.ws.get<float>((size_t)Mo * cw.cout);
+    float2* rp = R.ws.get<float2>((size_t)Mo * (cw.cout / seg));
+    float2* st = R.ws.get<float2>((size_t)n * G);
+    if (stage > 0) {
+      s = plain_src(raw, C);
+      s.stats = stats;
+      s.gamma = m->vg[stage - 1].p;
+      s.beta = m->vb[stage - 1].p;
+      s.G = G;
+      s.act = 1;
+      mode = SRC_GNACT;
+    }
+    gemm(R, s, mode, n, H, W, cw, EPI_STATS, r, nullptr, rp, seg);
+    gn_finalize(R, rp, st, n, Ho * Wo, cw.cout / seg, G, cw.cout);
+    raw = r;
+    stats = st;
+    C = cw.cout;
+    H = Ho;
+    W = Wo;
+  }
+  float* act = R.ws.get<float>((size_t)n * H * W * C);
+  FinishParams fp;
+  std::memset(&fp, 0, sizeof(fp));
+  fp.raw = raw;
+  fp.stats = stats;
+  fp.gamma = m->vg[5].p;
+  fp.beta = m->vb[5].p;
+  fp.G = G;
+  fp.C = C;
+  fp.H = H;
+  fp.W = W;
+  fp.N = n;
+  fp.act = 1;
+  fp.out = act;
+  finish(R, fp, SRC_PLAIN);
+  if (R.plan) return;
+  dim3 grid(cdiv(H * W, 256), n);
+  vae_tail_kernel<<<grid, 256, 0, R.st>>>(act, m->vconv[3].B, m->vconv[3].bias, n, H, W, img, u8);
+  HIPCHK(hipGetLastError());
+}
+
+}  // namespace dmx
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+using namespace dmx;
+
+template <typename F>
+static int guarded(F&& f) {
+  try {
+    f();
+    return DMX_OK;
+  } catch (const Error& e) {
+    g_err = e.what();
+    return e.code;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return DMX_E_INTERNAL;
+  } catch (...) {
+    g_err = "unknown error";
+    return DMX_E_INTERNAL;
+  }
+}
+
+extern "C" {
+
+int dmx_abi_version(void) { return 1; }
+const char* dmx_last_error(void) { return g_err.c_str(); }
+
+int dmx_create(int device, dmx_ctx** out) {
+  return guarded([&] {
+    REQUIRE(out != nullptr, "null out");
+    HIPCHK(hipSetDevice(device));
+    auto* c = new dmx_ctx();
+    c->device = device;
+    *out = c;
+  });
+}
+
+int dmx_destroy(dmx_ctx* ctx) {
+  return guarded([&] {
+    if (!ctx) return;
+    if (ctx->pos_table) (void)hipFree(ctx->pos_table);
+    delete ctx;
+  });
+}
+
+int dmx_set_time_table(dmx_ctx* ctx, const float* host_table, int tmax) {
+  return guarded([&] {
+    REQUIRE(ctx && host_table && tmax >= 1, "bad time table");
+    if (ctx->pos_table) HIPCHK(hipFree(ctx->pos_table));
+    ctx->pos_table = nullptr;
+    HIPCHK(hipMalloc(&ctx->pos_table, (size_t)tmax * 256 * sizeof(float)));
+    HIPCHK(hipMemcpy(ctx->pos_table, host_table, (size_t)tmax * 256 * sizeof(float), hipMemcpyHostToDevice));
+    ctx->tmax = tmax;
+  });
+}
+
+int dmx_model_num_keys(int kind, int in_ch, int remove_deep_conv) {
+  if (kind < DMX_UNET_COND_GEOM || kind > DMX_VAE) return -1;
+  return (int)model_keys(kind, in_ch, !remove_deep_conv).size();
+}
+
+int dmx_model_key(int kind, int in_ch, int remove_deep_conv, int index, char* name_out, int name_cap,
+                  int64_t* shape_out, int* ndim_out) {
+  return guarded([&] {
+    Keys k = model_keys(kind, in_ch, !remove_deep_conv);
+    REQUIRE(index >= 0 && index < (int)k.size(), "key index out of range");
+    REQUIRE(name_out && name_cap > (int)k[index].name.size(), "name buffer too small");
+    std::strcpy(name_out, k[index].name.c_str());
+    if (ndim_out) *ndim_out = (int)k[index].shape.size();
+    if (shape_out)
+      for (size_t i = 0; i < k[index].shape.size() && i < 4; ++i) shape_out[i] = k[index].shape[i];
+  });
+}
+
+int dmx_model_create(dmx_ctx* ctx, int kind, int in_ch, int remove_deep_conv, dmx_model** out) {
+  return guarded([&] {
+    REQUIRE(ctx && out, "null argument");
+    REQUIRE(kind >= DMX_UNET_COND_GEOM && kind <= DMX_VAE, "unknown model kind");
+    REQUIRE(in_ch >= 1 && in_ch <= 4, "in_ch must be in [1,4]");
+    auto* m = new dmx_model();
+    m->ctx = ctx;
+    m->kind = kind;
+    m->in_ch = in_ch;
+    m->deep = !remove_deep_conv;
+    m->keys = model_keys(kind, in_ch, m->deep);
+    *out = m;
+  });
+}
+
+int dmx_model_destroy(dmx_model* m) {
+  return guarded([&] {
+    if (!m) return;
+    if (m->has_graph) {
+      (void)hipGraphExecDestroy(m->gexec);
+      (void)hipGraphDestroy(m->graph);
+    }
+    for (void* p : m->owned) (void)hipFree(p);
+    if (m->ws_mem) (void)hipFree(m->ws_mem);
+    delete m;
+  });
+}
+
+int dmx_model_set_tensor(dmx_model* m, const char* name, const float* dev_ptr, const int64_t* shape, int ndim) {
+  return guarded([&] {
+    REQUIRE(m && name && dev_ptr && (ndim == 0 || shape), "null argument");
+    REQUIRE(ndim >= 0 && ndim <= 4, "ndim must be <= 4");
+    std::vector<int64_t> s(shape, shape + ndim);
+    bool known = false;
+    for (auto& k : m->keys)
+      if (k.name == name) {
+        known = true;
+        if (k.shape != s) throw Error(DMX_E_ARG, std::string("shape mismatch for '") + name + "'");
+      }
+    if (!known) throw Error(DMX_E_ARG, std::string("unexpected key '") + name + "'");
+    m->inputs[name] = {dev_ptr, s};
+  });
+}
+
+int dmx_model_finalize(dmx_model* m, void* stream) {
+  return guarded([&] {
+    REQUIRE(m, "null model");
+    finalize_model(m, (hipStream_t)stream);
+  });
+}
+
+int64_t dmx_model_workspace_bytes(const dmx_model* m) { return m ? (int64_t)m->ws_cap : -1; }
+
+int dmx_debug_enable(dmx_model* m, int on) {
+  return guarded([&] {
+    REQUIRE(m != nullptr, "null model");
+    m->debug = on != 0;
+    m->taps.clear();
+  });
+}
+
+int dmx_debug_num_taps(const dmx_model* m) { return m ? (int)m->taps.size() : -1; }
+
+int dmx_debug_tap(dmx_model* m, int i, char* name_out, int cap, int64_t* count_out, float* dst, void* stream) {
+  return guarded([&] {
+    REQUIRE(m && i >= 0 && i < (int)m->taps.size(), "bad tap index");
+    auto& t = m->taps[i];
+    REQUIRE(name_out && cap > (int)t.first.size(), "name buffer too small");
+    std::strcpy(name_out, t.first.c_str());
+    if (count_out) *count_out = (int64_t)t.second.second;
+    if (dst)
+      HIPCHK(hipMemcpyAsync(dst, t.second.first, t.second.second * sizeof(float), hipMemcpyDeviceToDevice,
+                            (hipStream_t)stream));
+  });
+}
+
+int dmx_unet_forward(dmx_model* m, const float* x, const int64_t* t, const int64_t* y, const float* vals,
+                     const float* mask, float* eps, float* geom, int n, int h, int w, void* stream) {
+  return guarded([&] {
+    REQUIRE(m != nullptr, "null model");
+    check_shapes(m, n, h, w);
+    REQUIRE(x && t && eps, "null tensor");
+    if (m->kind != DMX_UNET) REQUIRE(y != nullptr, "conditional U-Net needs y");
+    REQUIRE((vals == nullptr) == (mask == nullptr), "vals and mask must be given together");
+    REQUIRE(geom == nullptr || m->kind == DMX_UNET_COND_GEOM, "geom output only for UnetCondWithGeomHead");
+    hipStream_t st = (hipStream_t)stream;
+    m->taps.clear();
+    run_planned(m, st, [&](Run& R) {
+      FwdIn in{x, n, t, 1, y, 0, 0, vals, mask, n};
+      float* feat = unet_trunk(R, in, n, h, w);
+      if (R.plan) return;
+      dim3 grid(cdiv(h * w, 256), n);
+      out_head_kernel<<<grid, 256, 0, st>>>(feat, m->out_w, m->out_b, eps, m->in_ch, h * w);
+      HIPCHK(hipGetLastError());
+      if (geom) {
+        geom_head_kernel<<<n, 256, 0, st>>>(feat, h * w, m->gw0, m->gb0, m->gw2, m->gb2, 12, geom);
+        HIPCHK(hipGetLastError());
+      }
+    });
+  });
+}
+
+int dmx_step(dmx_model* m, const dmx_step_args* a, void* stream) {
+  return guarded([&] {
+    REQUIRE(m != nullptr, "null model");
+    validate_step(m, a);
+    run_planned(m, (hipStream_t)stream, [&](Run& R) { step_body(R, *a); });
+  });
+}
+
+int dmx_sample_loop(dmx_model* m, const dmx_step_args* a, int steps, int use_graph, void* stream) {
+  return guarded([&] {
+    REQUIRE(m != nullptr, "null model");
+    validate_step(m, a);
+    REQUIRE(a->x_in == a->x_out, "sample loop runs in place (x_in == x_out)");
+    REQUIRE(a->t_stride == 0, "sample loop needs a device scalar t (t_stride 0)");
+    REQUIRE(a->noise == nullptr, "sample loop draws on-device Philox noise (noise must be NULL)");
+    REQUIRE(steps >= 0, "steps must be >= 0");
+    hipStream_t st = (hipStream_t)stream;
+    int64_t* tdev = const_cast<int64_t*>(a->t);
+    if (!use_graph) {
+      for (int i = 0; i < steps; ++i) {
+        run_planned(m, st, [&](Run& R) { step_body(R, *a); });
+        decrement_t_kernel<<<1, 64, 0, st>>>(tdev);
+        HIPCHK(hipGetLastError());
+      }
+      return;
+    }
+    GraphKey key;
+    std::memset(&key, 0, sizeof(key));
+    std::memcpy(&key.a, a, sizeof(dmx_step_args));
+    if (!(m->has_graph && key == m->gkey)) {
+      if (m->has_graph) {
+        (void)hipGraphExecDestroy(m->gexec);
+        (void)hipGraphDestroy(m->graph);
+        m->has_graph = false;
+      }
+      // plan + allocate outside capture, then capture the real launches
+      m->ws.base = nullptr;
+      m->ws.off = 0;
+      m->ws.plan = true;
+      {
+        Run P{m, st, true, m->ws};
+        step_body(P, *a);
+      }
+      ensure_ws(m);
+      m->ws.base = static_cast<char*>(m->ws_mem);
+      m->ws.off = 0;
+      m->ws.plan = false;
+      HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+      try {
+        Run R{m, st, false, m->ws};
+        step_body(R, *a);
+        decrement_t_kernel<<<1, 64, 0, st>>>(tdev);
+      } catch (...) {
+        hipGraph_t g;
+        (void)hipStreamEndCapture(st, &g);
+        if (g) (void)hipGraphDestroy(g);
+        throw;
+      }
+      HIPCHK(hipStreamEndCapture(st, &m->graph));
+      HIPCHK(hipGraphInstantiate(&m->gexec, m->graph, nullptr, nullptr, 0));
+      m->gkey = key;
+      m->has_graph = true;
+    }
+    for (int i = 0; i < steps; ++i) HIPCHK(hipGraphLaunch(m->gexec, st));
+  });
+}
+
+int dmx_step_profile(dmx_model* m, const dmx_step_args* a, dmx_kernel_record* recs, int cap, int* n_out,
+                     void* stream) {
+  return guarded([&] {
+    REQUIRE(m != nullptr && recs != nullptr && n_out != nullptr, "null argument");
+    validate_step(m, a);
+    hipStream_t st = (hipStream_t)stream;
+    Prof prof;
+    m->ws.base = nullptr;
+    m->ws.off = 0;
+    m->ws.plan = true;
+    {
+      Run P{m, st, true, m->ws};
+      step_body(P, *a);
+    }
+    ensure_ws(m);
+    m->ws.base = static_cast<char*>(m->ws_mem);
+    m->ws.off = 0;
+    m->ws.plan = false;
+    Run R{m, st, false, m->ws, &prof};
+    step_body(R, *a);
+    HIPCHK(hipStreamSynchronize(st));
+    int n = 0;
+    for (auto& r : prof.recs) {
+      if (n >= cap) break;
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, r.e0, r.e1));
+      std::memset(&recs[n], 0, sizeof(recs[n]));
+      std::snprintf(recs[n].kernel, sizeof recs[n].kernel, "%s", r.kernel.c_str());
+      std::snprintf(recs[n].layer, sizeof recs[n].layer, "%s", r.layer.c_str());
+      recs[n].flops = r.flops;
+      recs[n].bytes = r.bytes;
+      recs[n].ms = ms;
+      ++n;
+    }
+    *n_out = n;
+  });
+}
+
+int dmx_ddpm_update(const float* x, float* x_out, const float* eu, const float* ec, float guidance,
+                    const int64_t* t, int t_stride, const float* c1, const float* c2, const float* sd, int T,
+                    const float* noise, uint64_t seed, int64_t sample_offset, int n, int c, int h, int w,
+                    void* stream) {
+  return guarded([&] {
+    REQUIRE(x && x_out && eu && t && c1 && c2 && sd, "null tensor");
+    REQUIRE(n >= 1 && c >= 1 && c <= 4 && h >= 1 && w >= 1 && T >= 1, "bad shape");
+    StepTailParams p;
+    std::memset(&p, 0, sizeof(p));
+    p.Co = c;
+    p.B = n;
+    p.HW = h * w;
+    p.cfg = ec != nullptr ? 1 : 0;
+    p.guidance = guidance;
+    p.eps_u = eu;
+    p.eps_c = ec;
+    p.x = x;
+    p.x_out = x_out;
+    p.t = t;
+    p.t_stride = t_stride;
+    p.tmax = T;
+    p.c1 = c1;
+    p.c2 = c2;
+    p.sd = sd;
+    p.noise = noise;
+    p.seed = seed;
+    p.sample_offset = sample_offset;
+    dim3 grid(cdiv(p.HW, 256), n);
+    step_tail_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(p);
+    HIPCHK(hipGetLastError());
+  });
+}
+
+int dmx_vae_decode(dmx_model* m, const float* z, float* img, uint8_t* u8, int n, int h, int w, void* stream) {
+  return guarded([&] {
+    REQUIRE(m != nullptr, "null model");
+    if (!m->finalized) throw Error(DMX_E_STATE, "model weights not finalized");
+    REQUIRE(m->kind == DMX_VAE, "not a VAE model");
+    REQUIRE(z && (img || u8), "null tensor");
+    REQUIRE(n >= 1 && h >= 1 && w >= 1, "bad shape");
+    const int chunk = 16;  // bounds workspace (the reference decodes in chunks of 4, diff.py:353)
+    hipStream_t st = (hipStream_t)stream;
+    for (int s = 0; s < n; s += chunk) {
+      const int b = std::min(chunk, n - s);
+      run_planned(m, st, [&](Run& R) {
+        vae_body(R, z + (size_t)s * 4 * h * w, img ? img + (size_t)s * 3 * 64 * h * w : nullptr,
+                 u8 ? u8 + (size_t)s * 64 * h * w * 3 : nullptr, b, h, w);
+      });
+    }
+  });
+}
+
+}  // extern "C"

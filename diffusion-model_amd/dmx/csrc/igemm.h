@@ -1,0 +1,184 @@
+// dmx — implicit GEMM on fp32 MFMA (v_mfma_f32_32x32x2_f32) for gfx950.
+//
+//   C[m, n] = sum_k A[m, k] * B[n, k]      m: output pixel/token, n: out channel
+//
+// One kernel serves conv3x3 (9 taps), each phase of ConvTranspose 4x4/s2
+// (4 taps per phase, blockIdx.z = phase) and token Linear layers (1 tap).
+// A is gathered on the fly from a fused source (source.h: plain NHWC,
+// GroupNorm+GELU of a raw conv output, 2x2 max-pool, bilinear-x2+pad+concat,
+// NCHW input); B is the repacked weight [phase][Npad][Kpad] (k contiguous,
+// k = tap * C + c).  fp32 in / fp32 accumulate: each MFMA is bit-for-bit an
+// fmaf chain, so no precision is traded for the matrix cores.
+//
+// Tiling: 256 threads = 4 waves in a 2x2 grid; block tile BM x BN, K-step 16,
+// LDS double buffer (rows padded to 20 floats => conflict-free ds_read_b128),
+// register-staged global loads for tile k+1 issued before the MFMAs of tile k.
+// Inside a K-step lane (r, h) feeds k = 8h + s to MFMA s, so every fragment is
+// two contiguous ds_read_b128 (the k order inside an MFMA is free as long as A
+// and B agree).
+#pragma once
+#include "common.h"
+#include "source.h"
+
+namespace dmx {
+
+struct IgemmParams {
+  SrcDesc src;
+  int H, W;           // GEMM row grid (input grid of the conv / token grid)
+  int M;              // rows = N * H * W
+  int taps;
+  int8_t dy[4][9], dx[4][9];  // tap offsets per phase
+  int Kreal, Kpad;
+  int Cout, Npad;
+  int osy, osx;       // output stride (2 for ConvT phases)
+  int Hout, Wout;
+  int8_t py[4], px[4];  // output offset per phase
+  const float* Bw;    // [phases][Npad][Kpad]
+  const float* bias;  // [Cout] or null
+  float* out;         // NHWC [N][Hout][Wout][Cout]
+  const float* res;   // EPI_BIAS_RES residual, same layout as out
+  float2* rowpart;    // EPI_STATS: [N*Hout*Wout][Cout/seg]
+  int seg;            // columns per GroupNorm partial (power of two, <= 32)
+};
+
+constexpr int IG_BK = 16;
+constexpr int IG_LDS_STRIDE = 20;  // floats per LDS row (16 + 4 pad)
+
+template <int BM, int BN, int SRC, int EPI>
+__global__ __launch_bounds__(256) void igemm_f32_kernel(const IgemmParams p) {
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
+  constexpr int AP = BM * 4 / 256, BP = BN * 4 / 256;
+  static_assert(TM >= 1 && TN >= 1 && AP >= 1 && BP >= 1, "tile");
+
+  __shared__ __attribute__((aligned(16))) float As[2][BM][IG_LDS_STRIDE];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN][IG_LDS_STRIDE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int phase = blockIdx.z;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int q = tid & 3;          // float4 piece within a 16-wide K slice
+  const int rbase = tid >> 2;     // staging row (+ i * 64)
+  const float* Bw = p.Bw + (size_t)phase * p.Npad * p.Kpad;
+  const int HW = p.H * p.W;
+  const int C = p.src.C;
+
+  // per staged A row: decode m -> (n, y, x) once
+  int an[AP], ay[AP], ax[AP];
+  bool av[AP];
+#pragma unroll
+  for (int i = 0; i < AP; ++i) {
+    const int m = m0 + rbase + i * 64;
+    av[i] = m < p.M;
+    const int mm = av[i] ? m : 0;
+    an[i] = mm / HW;
+    const int r = mm - an[i] * HW;
+    ay[i] = r / p.W;
+    ax[i] = r - ay[i] * p.W;
+  }
+
+  floatx4 ra[AP], rb[BP];
+  auto load_tile = [&](int kt) {
+    const int k = kt * IG_BK + q * 4;
+    const bool kv = k < p.Kreal;
+    const int tap = kv ? k / C : 0;
+    const int c = k - tap * C;
+    const int ddy = p.dy[phase][tap], ddx = p.dx[phase][tap];
+#pragma unroll
+    for (int i = 0; i < AP; ++i) {
+      const int iy = ay[i] + ddy, ix = ax[i] + ddx;
+      const bool ok = kv && av[i] && iy >= 0 && ix >= 0 && iy < p.H && ix < p.W;
+      ra[i] = ok ? load_src4<SRC>(p.src, an[i], iy, ix, c, p.H, p.W) : floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < BP; ++i)
+      rb[i] = ld4(Bw + (size_t)(n0 + rbase + i * 64) * p.Kpad + kt * IG_BK + q * 4);
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < AP; ++i) *reinterpret_cast<floatx4*>(&As[buf][rbase + i * 64][q * 4]) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BP; ++i) *reinterpret_cast<floatx4*>(&Bs[buf][rbase + i * 64][q * 4]) = rb[i];
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nK = p.Kpad / IG_BK;
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+
+  const int fr = lane & 31, fh = lane >> 5;
+  for (int kt = 0; kt < nK; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nK) load_tile(kt + 1);
+    floatx4 a[TM][2], b[TN][2];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const float* ap = &As[buf][wm * WM + i * 32 + fr][8 * fh];
+      a[i][0] = ld4(ap);
+      a[i][1] = ld4(ap + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float* bp = &Bs[buf][wn * WN + j * 32 + fr][8 * fh];
+      b[j][0] = ld4(bp);
+      b[j][1] = ld4(bp + 4);
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i][s >> 2][s & 3], b[j][s >> 2][s & 3], acc[i][j], 0, 0, 0);
+    if (kt + 1 < nK) store_tile(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue -------------------------------------------------------------
+  const int HWo = p.Hout * p.Wout;
+  const int nseg = p.Cout / (EPI == EPI_STATS ? p.seg : 1);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * fh;
+      const int m = m0 + wm * WM + i * 32 + row;
+      const bool mv = m < p.M;
+      size_t oidx = 0;
+      if (mv) {
+        const int nn = m / HW, rr = m - nn * HW, y = rr / p.W, x = rr - y * p.W;
+        oidx = ((size_t)nn * p.Hout + (y * p.osy + p.py[phase])) * p.Wout + (x * p.osx + p.px[phase]);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * WN + j * 32 + fr;
+        const bool v = mv && col < p.Cout;
+        float val = acc[i][j][r];
+        if (p.bias != nullptr && col < p.Cout) val += p.bias[col];
+        if constexpr (EPI == EPI_BIAS_GELU) val = gelu(val);
+        if constexpr (EPI == EPI_BIAS_RES) {
+          if (v) val += p.res[oidx * p.Cout + col];
+        }
+        if (v) p.out[oidx * p.Cout + col] = val;
+        if constexpr (EPI == EPI_STATS) {
+          float s1 = v ? val : 0.f, s2 = v ? val * val : 0.f;
+          for (int o = 1; o < p.seg; o <<= 1) {
+            s1 += __shfl_xor(s1, o, 64);
+            s2 += __shfl_xor(s2, o, 64);
+          }
+          if (v && (fr & (p.seg - 1)) == 0) p.rowpart[oidx * nseg + col / p.seg] = make_float2(s1, s2);
+        }
+      }
+    }
+  }
+}
+
+}  // namespace dmx

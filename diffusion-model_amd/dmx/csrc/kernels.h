@@ -1,0 +1,565 @@
+// dmx — non-GEMM device kernels of the CFG denoising step and the VAE decoder.
+#pragma once
+#include "common.h"
+#include "source.h"
+
+namespace dmx {
+
+// ---------------------------------------------------------------------------
+// Wave / block reductions (wave64)
+// ---------------------------------------------------------------------------
+DMX_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// K2 embed: emb = pos(t) + class_emb[y] (+ cond_mlp([vals, mask])), then all six
+// per-block heads SiLU -> Linear(256 -> C_i) concatenated into one row.
+// Reference: models/unet_cond.py:155-167 (pos/class), 125-129 (cond_mlp),
+// 62-65/82-85 (emb_layer), models/unet_cond_geom.py:89-95, models/unet.py:167-170.
+// pos_table[t-1][k] is computed on the host by torch (bit-exact with the
+// reference's fp32 sin/cos); one 256-thread block per sample.
+// ---------------------------------------------------------------------------
+struct EmbedParams {
+  const int64_t* t; int t_stride; int tmax;
+  int t_mod;                   // CFG batching: sample n reads t[n % t_mod] (0 => t[n])
+  const int64_t* y;            // null => no class embedding (unconditional Unet)
+  int y_null_first;            // CFG batching: samples [0, n_half) use y = y_null
+  int64_t y_null; int n_half;
+  const float* vals; const float* mask;  // (n_half or n, 12) or null
+  int cond_rows;               // rows of vals/mask (n or n_half => row = n % n_half)
+  const float* pos_table;      // [tmax][256]
+  const float* class_emb;      // [ncls][256]
+  int ncls;
+  const float* w0; const float* b0;   // cond_mlp.0: [256][24]
+  const float* w2t; const float* b2;  // cond_mlp.2 transposed: [256 in][256 out]
+  const float* wht; const float* bh;  // heads transposed: [256][Hsum]
+  int hsum;
+  float* out;                  // [n][hsum]
+};
+
+__global__ __launch_bounds__(256) void embed_kernel(const EmbedParams p) {
+  __shared__ float e[256], s[256], h[256], in24[24];
+  const int n = blockIdx.x, k = threadIdx.x;
+  int64_t t = p.t[(size_t)(p.t_mod ? n % p.t_mod : n) * p.t_stride];
+  t = t < 1 ? 1 : (t > p.tmax ? p.tmax : t);
+  float v = p.pos_table[(size_t)(t - 1) * 256 + k];
+  if (p.y != nullptr) {
+    int64_t yy;
+    if (p.y_null_first) yy = (n < p.n_half) ? p.y_null : p.y[n - p.n_half];
+    else yy = p.y[n];
+    yy = yy < 0 ? 0 : (yy >= p.ncls ? p.ncls - 1 : yy);
+    v += p.class_emb[yy * 256 + k];
+  }
+  if (p.vals != nullptr) {
+    const int row = n % p.cond_rows;
+    if (k < 12) in24[k] = p.vals[row * 12 + k];
+    else if (k < 24) in24[k] = p.mask[row * 12 + (k - 12)];
+    __syncthreads();
+    float a = p.b0[k];
+#pragma unroll
+    for (int j = 0; j < 24; ++j) a += p.w0[k * 24 + j] * in24[j];
+    h[k] = silu(a);
+    __syncthreads();
+    float c = p.b2[k];
+    for (int j = 0; j < 256; ++j) c += p.w2t[j * 256 + k] * h[j];
+    v += c;
+  }
+  e[k] = v;
+  s[k] = silu(v);
+  __syncthreads();
+  for (int o = k; o < p.hsum; o += 256) {
+    float a = p.bh[o];
+    for (int j = 0; j < 256; ++j) a += p.wht[(size_t)j * p.hsum + o] * s[j];
+    p.out[(size_t)n * p.hsum + o] = a;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K4 GroupNorm finalize: (mean, rstd) per (n, g) from per-row partials written by
+// the conv epilogue.  Sums are combined in double (deterministic order).
+// nn.GroupNorm eps = 1e-5 (models/unet_cond.py:20, models/vae.py:36).
+// ---------------------------------------------------------------------------
+// Finalize with the channel count known (element count = HW * C / G).
+__global__ __launch_bounds__(256) void gn_finalize_kernel(const float2* rowpart, float2* stats, int HW, int nseg,
+                                                            int G, int C, float eps) {
+  const int ng = blockIdx.x, n = ng / G, g = ng % G;
+  const int spg = nseg / G;
+  const int cnt_rows = HW * spg;
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = threadIdx.x; i < cnt_rows; i += 256) {
+    const int r = i / spg, sg = g * spg + (i - r * spg);
+    const float2 v = rowpart[((size_t)n * HW + r) * nseg + sg];
+    s1 += (double)v.x;
+    s2 += (double)v.y;
+  }
+  __shared__ double r1[256], r2[256];
+  r1[threadIdx.x] = s1;
+  r2[threadIdx.x] = s2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      r1[threadIdx.x] += r1[threadIdx.x + o];
+      r2[threadIdx.x] += r2[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double cnt = (double)HW * (double)(C / G);
+    const double mean = r1[0] / cnt;
+    double var = r2[0] / cnt - mean * mean;
+    var = var < 0.0 ? 0.0 : var;
+    stats[ng] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)eps)));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// ResBlock / decoder-stage finish (materialises the block output, NHWC):
+//   y = GN(raw)                     (non-residual ResBlock, models/unet_cond.py:30)
+//   y = GELU(x + GN(raw))           (residual ResBlock, models/unet_cond.py:28)
+//   y = GELU(GN(raw))               (VAE GN+GELU, models/vae.py:36-48)
+//   y += emb[n][c]                  (Down/Up "+ emb", models/unet_cond.py:69-70,99-100)
+// The residual input x is re-derived from its fused source (max-pool, up+cat).
+// ---------------------------------------------------------------------------
+struct FinishParams {
+  const float* raw; const float2* stats; const float* gamma; const float* beta; int G;
+  int C, H, W, N;
+  SrcDesc res;       // residual source (valid if has_res)
+  int has_res;
+  int act;           // GELU after GN (no residual)
+  const float* emb; int emb_stride; int emb_off;
+  float* out;
+};
+
+template <int RSRC>
+__global__ __launch_bounds__(256) void finish_kernel(const FinishParams p) {
+  const int C4 = p.C / 4;
+  const size_t total = (size_t)p.N * p.H * p.W * C4;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const int c = (int)(i % C4) * 4;
+    const size_t pix = i / C4;
+    const int n = (int)(pix / ((size_t)p.H * p.W));
+    const int rr = (int)(pix - (size_t)n * p.H * p.W);
+    const int y = rr / p.W, x = rr - y * p.W;
+    floatx4 v = ld4(p.raw + pix * p.C + c);
+    const int g = c / (p.C / p.G);
+    floatx4 o = gn_apply4(v, p.stats[n * p.G + g], p.gamma, p.beta, c, 0);
+    if (p.has_res) {
+      floatx4 r = load_src4<RSRC>(p.res, n, y, x, c, p.H, p.W);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = gelu(r[j] + o[j]);
+    } else if (p.act) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = gelu(o[j]);
+    }
+    if (p.emb != nullptr) {
+      floatx4 e = ld4(p.emb + (size_t)n * p.emb_stride + p.emb_off + c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] += e[j];
+    }
+    *reinterpret_cast<floatx4*>(p.out + pix * p.C + c) = o;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LayerNorm over C per token (nn.LayerNorm eps=1e-5, models/unet_cond.py:37-39).
+// One wave per token, C in {64,128,256,512}: C/64 values per lane, two-pass.
+// ---------------------------------------------------------------------------
+template <int CPL>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* x, float* y, const float* w, const float* b,
+                                                        int M, float eps) {
+  constexpr int C = CPL * 64;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float* xr = x + (size_t)row * C;
+  float v[CPL];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    v[j] = xr[lane + 64 * j];
+    s += v[j];
+  }
+  const float mean = wave_sum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const float d = v[j] - mean;
+    q += d * d;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)C + eps);
+  float* yr = y + (size_t)row * C;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane + 64 * j;
+    yr[c] = (v[j] - mean) * rstd * w[c] + b[c];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K5 multi-head self-attention core, flash-style, fp32 MFMA 16x16x4.
+// qkv: [N][L][3C] (q | k | v, heads of width D inside each), out: [N][L][C].
+// softmax(q k^T / sqrt(D)) v per (sample, head)  (nn.MultiheadAttention, 4 heads,
+// models/unet_cond.py:36,49).  Computed transposed (S^T = K Q^T, O^T = V^T P^T) so
+// the query sits on the lane: the P accumulator is directly the B operand of PV.
+// Each wave owns 16*QT queries; 64-key K/V chunks are staged in LDS.
+// ---------------------------------------------------------------------------
+template <int D, int QT>
+__global__ __launch_bounds__(256) void attention_kernel(const float* qkv, float* out, int L, int C) {
+  constexpr int KC = 64, DS = D + 4, DP = D / 4;
+  __shared__ __attribute__((aligned(16))) float Ks[KC][DS];
+  __shared__ __attribute__((aligned(16))) float Vs[KC][DS];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int hd = blockIdx.y, n = blockIdx.z;
+  const int ql = lane & 15, g = lane >> 4;
+  const size_t rs = (size_t)3 * C;
+  const float* base = qkv + (size_t)n * L * rs;
+  const float scale = 1.0f / sqrtf((float)D);
+
+  float qf[QT][DP];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    const int qi = blockIdx.x * (64 * QT) + wid * 16 * QT + qt * 16 + ql;
+#pragma unroll
+    for (int s = 0; s < DP; ++s) qf[qt][s] = (qi < L) ? base[(size_t)qi * rs + hd * D + g * DP + s] * scale : 0.f;
+  }
+  floatx4 o[QT][D / 16];
+  float mrun[QT], lrun[QT];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    mrun[qt] = -INFINITY;
+    lrun[qt] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < D / 16; ++dt) o[qt][dt] = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  for (int c0 = 0; c0 < L; c0 += KC) {
+    // stage K, V chunk (zero beyond L)
+    for (int i = tid; i < KC * (D / 4); i += 256) {
+      const int key = i / (D / 4), d4 = (i % (D / 4)) * 4;
+      floatx4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
+      if (c0 + key < L) {
+        const float* r = base + (size_t)(c0 + key) * rs + hd * D + d4;
+        kv = ld4(r + C);
+        vv = ld4(r + 2 * C);
+      }
+      *reinterpret_cast<floatx4*>(&Ks[key][d4]) = kv;
+      *reinterpret_cast<floatx4*>(&Vs[key][d4]) = vv;
+    }
+    __syncthreads();
+    const int nvalid = L - c0;
+    floatx4 sc[QT][4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      float kf[DP];
+#pragma unroll
+      for (int s = 0; s < DP; ++s) kf[s] = Ks[kt * 16 + ql][g * DP + s];
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) {
+        floatx4 a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < DP; ++s) a = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[s], qf[qt][s], a, 0, 0, 0);
+        sc[qt][kt] = a;
+      }
+    }
+    // online softmax over this chunk (keys >= L masked)
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kt * 16 + g * 4 + r;
+          if (key >= nvalid) sc[qt][kt][r] = -INFINITY;
+          mx = fmaxf(mx, sc[qt][kt][r]);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(mrun[qt], mx);
+      const float alpha = expf(mrun[qt] - mnew);
+      float ls = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = expf(sc[qt][kt][r] - mnew);
+          sc[qt][kt][r] = pv;
+          ls += pv;
+        }
+      lrun[qt] = lrun[qt] * alpha + ls;
+      mrun[qt] = mnew;
+#pragma unroll
+      for (int dt = 0; dt < D / 16; ++dt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[qt][dt][r] *= alpha;
+    }
+    // O^T += V^T P^T
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float vf[D / 16];
+#pragma unroll
+        for (int dt = 0; dt < D / 16; ++dt) vf[dt] = Vs[kt * 16 + g * 4 + r][dt * 16 + ql];
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+          for (int dt = 0; dt < D / 16; ++dt)
+            o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vf[dt], sc[qt][kt][r], o[qt][dt], 0, 0, 0);
+      }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    float l = lrun[qt];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.0f / l;
+    const int qi = blockIdx.x * (64 * QT) + wid * 16 * QT + qt * 16 + ql;
+    if (qi < L) {
+#pragma unroll
+      for (int dt = 0; dt < D / 16; ++dt) {
+        floatx4 v = o[qt][dt];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] *= inv;
+        *reinterpret_cast<floatx4*>(out + ((size_t)n * L + qi) * C + hd * D + dt * 16 + g * 4) = v;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 counter RNG + Box-Muller -> 4 N(0,1) per counter (perf mode K8).
+// ---------------------------------------------------------------------------
+DMX_DEV uint4 philox4x32(uint4 ctr, uint2 key) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint32_t hi0 = __umulhi(0xD2511F53u, ctr.x), lo0 = 0xD2511F53u * ctr.x;
+    const uint32_t hi1 = __umulhi(0xCD9E8D57u, ctr.z), lo1 = 0xCD9E8D57u * ctr.z;
+    ctr = make_uint4(hi1 ^ ctr.y ^ key.x, lo1, hi0 ^ ctr.w ^ key.y, lo0);
+    key.x += 0x9E3779B9u;
+    key.y += 0xBB67AE85u;
+  }
+  return ctr;
+}
+
+DMX_DEV floatx4 normal4(uint64_t seed, uint64_t stream, uint64_t index) {
+  const uint4 r = philox4x32(make_uint4((uint32_t)index, (uint32_t)(index >> 32), (uint32_t)stream,
+                                        (uint32_t)(stream >> 32)),
+                             make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+  const float k = 2.3283064365386963e-10f;  // 2^-32
+  const float u1 = ((float)r.x + 0.5f) * k, u2 = ((float)r.y + 0.5f) * k;
+  const float u3 = ((float)r.z + 0.5f) * k, u4 = ((float)r.w + 0.5f) * k;
+  const float a = sqrtf(-2.0f * logf(u1)), b = sqrtf(-2.0f * logf(u3));
+  const float t1 = 6.283185307179586f * u2, t2 = 6.283185307179586f * u4;
+  return floatx4{a * cosf(t1), a * sinf(t1), b * cosf(t2), b * sinf(t2)};
+}
+
+// ---------------------------------------------------------------------------
+// K1/K6: out head (conv1x1 64->Co + bias) fused with the CFG mix and the DDPM
+// posterior step.  Reference: unet_cond.py:153 (out), diff.py:151 (CFG),
+// diff.py:141-144,158-162 (update).  The update arithmetic is performed with one
+// rounding per reference op, in the reference's op order, so given the same eps it
+// is bit-identical to torch-CPU:
+//   eps = eu + g*(ec - eu); mu = (x - c1[t]*eps) / c2[t]; x' = mu + noise*sd[t]
+// with c1 = (1-a)/sqrt(1-ab), c2 = sqrt(a), sd = sqrt((1-a)(1-ab_prev)/(1-ab))
+// tabulated on the host by torch.  noise = 0 where t == 1.
+// feat: [2B or B][H][W][64] NHWC; x, x_out, noise: NCHW [B][Co][H][W].
+// ---------------------------------------------------------------------------
+struct StepTailParams {
+  const float* feat; const float* w; const float* b;  // w: [Co][64]
+  int Co, B, HW, cfg;                                 // cfg: feat holds [uncond B | cond B]
+  float guidance;
+  const float* eps_u; const float* eps_c;             // alternative: precomputed eps (NCHW), feat null
+  const float* x; float* x_out;
+  const int64_t* t; int t_stride; int tmax;
+  const float* c1; const float* c2; const float* sd;  // [tmax], index t-1
+  const float* noise;                                 // NCHW or null => Philox
+  uint64_t seed; int64_t sample_offset;
+};
+
+#pragma clang fp contract(off)
+DMX_DEV float ddpm_elem(float x, float eps, float c1, float c2, float sd, float nz) {
+  const float mu = __fdiv_rn(__fsub_rn(x, __fmul_rn(c1, eps)), c2);
+  return __fadd_rn(mu, __fmul_rn(nz, sd));
+}
+
+__global__ __launch_bounds__(256) void step_tail_kernel(const StepTailParams p) {
+  const int pix = blockIdx.x * 256 + threadIdx.x;
+  const int n = blockIdx.y;
+  if (pix >= p.HW) return;
+  int64_t t = p.t[(size_t)n * p.t_stride];
+  t = t < 1 ? 1 : (t > p.tmax ? p.tmax : t);
+  float eu[4], ec[4];
+  const int Co = p.Co;
+  if (p.feat != nullptr) {
+    const float* fu = p.feat + ((size_t)n * p.HW + pix) * 64;
+    const float* fc = p.feat + ((size_t)(n + p.B) * p.HW + pix) * 64;
+    for (int c = 0; c < Co; ++c) {
+      eu[c] = p.b[c];
+      ec[c] = p.b[c];
+    }
+    for (int k = 0; k < 64; k += 4) {
+      const floatx4 a = ld4(fu + k);
+      floatx4 bb = {0.f, 0.f, 0.f, 0.f};
+      if (p.cfg) bb = ld4(fc + k);
+      for (int c = 0; c < Co; ++c) {
+        const floatx4 w = ld4(p.w + c * 64 + k);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          eu[c] = __fadd_rn(eu[c], __fmul_rn(w[j], a[j]));
+          ec[c] = __fadd_rn(ec[c], __fmul_rn(w[j], bb[j]));
+        }
+      }
+    }
+  } else {
+    for (int c = 0; c < Co; ++c) {
+      eu[c] = p.eps_u[((size_t)n * Co + c) * p.HW + pix];
+      ec[c] = p.cfg ? p.eps_c[((size_t)n * Co + c) * p.HW + pix] : 0.f;
+    }
+  }
+  float nz[4] = {0.f, 0.f, 0.f, 0.f};
+  if (t != 1) {
+    if (p.noise != nullptr) {
+      for (int c = 0; c < Co; ++c) nz[c] = p.noise[((size_t)n * Co + c) * p.HW + pix];
+    } else {
+      const floatx4 r = normal4(p.seed, (uint64_t)t, ((uint64_t)(n + p.sample_offset) * p.HW + pix));
+      for (int c = 0; c < Co && c < 4; ++c) nz[c] = r[c];
+    }
+  }
+  const float c1 = p.c1[t - 1], c2 = p.c2[t - 1], sd = p.sd[t - 1];
+  for (int c = 0; c < Co; ++c) {
+    const float eps = p.cfg ? __fadd_rn(eu[c], __fmul_rn(p.guidance, __fsub_rn(ec[c], eu[c]))) : eu[c];
+    const size_t idx = ((size_t)n * Co + c) * p.HW + pix;
+    p.x_out[idx] = ddpm_elem(p.x[idx], eps, c1, c2, sd, nz[c]);
+  }
+}
+
+// conv1x1 64 -> Co + bias into NCHW (models/unet_cond.py:153, the `out` layer).
+__global__ __launch_bounds__(256) void out_head_kernel(const float* feat, const float* w, const float* b, float* eps,
+                                                       int Co, int HW) {
+  const int pix = blockIdx.x * 256 + threadIdx.x, n = blockIdx.y;
+  if (pix >= HW) return;
+  const float* f = feat + ((size_t)n * HW + pix) * 64;
+  float acc[4];
+  for (int c = 0; c < Co; ++c) acc[c] = b[c];
+  for (int k = 0; k < 64; k += 4) {
+    const floatx4 a = ld4(f + k);
+    for (int c = 0; c < Co; ++c) {
+      const floatx4 ww = ld4(w + c * 64 + k);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[c] = __fadd_rn(acc[c], __fmul_rn(ww[j], a[j]));
+    }
+  }
+  for (int c = 0; c < Co; ++c) eps[((size_t)n * Co + c) * HW + pix] = acc[c];
+}
+
+// GeomHead: GAP over HW of feat (64 ch) -> Linear(64->256) -> SiLU -> Linear(256->12)
+// (models/unet_cond_geom.py:8-23).  One block per sample.
+__global__ __launch_bounds__(256) void geom_head_kernel(const float* feat, int HW, const float* w0, const float* b0,
+                                                        const float* w2, const float* b2, int gdim, float* geom) {
+  __shared__ float part[4][64], g[64], h[256];
+  const int n = blockIdx.x, tid = threadIdx.x, c = tid & 63, sl = tid >> 6;
+  float s = 0.f;
+  for (int pix = sl; pix < HW; pix += 4) s += feat[((size_t)n * HW + pix) * 64 + c];
+  part[sl][c] = s;
+  __syncthreads();
+  if (tid < 64) g[tid] = (part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid]) / (float)HW;
+  __syncthreads();
+  float a = b0[tid];
+  for (int k = 0; k < 64; ++k) a += w0[tid * 64 + k] * g[k];
+  h[tid] = silu(a);
+  __syncthreads();
+  if (tid < gdim) {
+    float o = b2[tid];
+    for (int k = 0; k < 256; ++k) o += w2[tid * 256 + k] * h[k];
+    geom[n * gdim + tid] = o;
+  }
+}
+
+// VAE tail: conv3x3 64->3 + bias (dec.18) -> sigmoid (models/vae.py:49,69), then
+// diff.py:58-62's x*255 -> clamp(0,255) -> uint8 (truncation), HWC for PIL.
+// in: materialised GELU(GN(dec.15)) NHWC [N][H][W][64].
+__global__ __launch_bounds__(256) void vae_tail_kernel(const float* in, const float* w, const float* b, int N, int H,
+                                                       int W, float* img, uint8_t* u8) {
+  __shared__ float ws[9 * 64 * 3];  // [tap][c][co]
+  for (int i = threadIdx.x; i < 9 * 64 * 3; i += 256) {
+    const int co = i % 3, c = (i / 3) % 64, tap = i / 192;
+    ws[i] = w[(co * 64 + c) * 9 + tap];
+  }
+  __syncthreads();
+  const int pix = blockIdx.x * 256 + threadIdx.x, n = blockIdx.y;
+  if (pix >= H * W) return;
+  const int y = pix / W, x = pix - y * W;
+  float a0 = b[0], a1 = b[1], a2 = b[2];
+  for (int tap = 0; tap < 9; ++tap) {
+    const int iy = y + tap / 3 - 1, ix = x + tap % 3 - 1;
+    if (iy < 0 || ix < 0 || iy >= H || ix >= W) continue;
+    const float* src = in + (((size_t)n * H + iy) * W + ix) * 64;
+    const float* wt = ws + tap * 192;
+    for (int c = 0; c < 64; c += 4) {
+      const floatx4 v = ld4(src + c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a0 += v[j] * wt[(c + j) * 3 + 0];
+        a1 += v[j] * wt[(c + j) * 3 + 1];
+        a2 += v[j] * wt[(c + j) * 3 + 2];
+      }
+    }
+  }
+  const float o[3] = {1.f / (1.f + expf(-a0)), 1.f / (1.f + expf(-a1)), 1.f / (1.f + expf(-a2))};
+  for (int co = 0; co < 3; ++co) {
+    if (img != nullptr) img[((size_t)n * 3 + co) * H * W + pix] = o[co];
+    if (u8 != nullptr) {
+      float q = __fmul_rn(o[co], 255.f);
+      q = fminf(fmaxf(q, 0.f), 255.f);
+      u8[((size_t)n * H * W + pix) * 3 + co] = (uint8_t)q;
+    }
+  }
+}
+
+// Weight repack into the implicit-GEMM B layout [phase][Npad][Kpad] (zero pad).
+//   kind 0: Conv2d [Cout][Cin][KS][KS], k = (ky*KS+kx)*Cin + c
+//   kind 1: Linear [Cout][Cin],        k = c
+//   kind 2: ConvTranspose2d(4,s2,p1) [Cin][Cout][4][4], phase (py,px), tap (jy,jx)
+__global__ void repack_kernel(float* dst, const float* src, int kind, int P, int Npad, int Kpad, int Cout, int Cin,
+                              int KS) {
+  const size_t total = (size_t)P * Npad * Kpad;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int k = (int)(i % Kpad), nn = (int)((i / Kpad) % Npad), ph = (int)(i / ((size_t)Kpad * Npad));
+    float v = 0.f;
+    if (kind == 0) {
+      if (nn < Cout && k < KS * KS * Cin) {
+        const int tap = k / Cin, c = k % Cin;
+        v = src[(((size_t)nn * Cin + c) * KS + tap / KS) * KS + tap % KS];
+      }
+    } else if (kind == 1) {
+      if (nn < Cout && k < Cin) v = src[(size_t)nn * Cin + k];
+    } else {
+      if (nn < Cout && k < 4 * Cin) {
+        const int j = k / Cin, c = k % Cin, jy = j >> 1, jx = j & 1, py = ph >> 1, px = ph & 1;
+        const int ky = py == 0 ? (jy == 0 ? 1 : 3) : (jy == 0 ? 0 : 2);
+        const int kx = px == 0 ? (jx == 0 ? 1 : 3) : (jx == 0 ? 0 : 2);
+        v = src[(((size_t)c * Cout + nn) * 4 + ky) * 4 + kx];
+      }
+    }
+    dst[i] = v;
+  }
+}
+
+// Transpose [R][Cc] -> [Cc][R] (embedding weights for coalesced access).
+__global__ void transpose_kernel(float* dst, const float* src, int R, int Cc) {
+  const size_t total = (size_t)R * Cc;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / Cc), c = (int)(i % Cc);
+    dst[(size_t)c * R + r] = src[i];
+  }
+}
+
+__global__ void decrement_t_kernel(int64_t* t) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *t = *t - 1;
+}
+
+}  // namespace dmx

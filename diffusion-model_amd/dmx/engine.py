@@ -1,0 +1,235 @@
+"""Python side of the native engine: contexts, weight loading, step / loop / decode.
+
+All arithmetic happens in libdmx.so (HIP kernels for gfx950).  This module only
+moves pointers: torch provides device memory and streams.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import StepArgs, check
+
+TIME_DIM = 256
+
+
+def pos_table(tmax: int) -> torch.Tensor:
+    """pos[t-1] for t = 1..tmax with the reference's exact fp32 formula
+    (models/unet_cond.py:155-161: long t repeated, times the fp32 inv_freq, sin|cos)."""
+    inv_freq = 1.0 / (10000 ** (torch.arange(0, TIME_DIM, 2).float() / TIME_DIM))
+    t = torch.arange(1, tmax + 1, dtype=torch.long).unsqueeze(-1)
+    tt = t.repeat(1, TIME_DIM // 2) * inv_freq
+    return torch.cat([torch.sin(tt), torch.cos(tt)], dim=-1).contiguous()
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class Context:
+    """One dmx_ctx per device per process."""
+
+    _ctxs: Dict[int, "Context"] = {}
+    _lock = threading.Lock()
+
+    def __init__(self, index: int):
+        self.lib = _lib.load()
+        self.index = index
+        h = ctypes.c_void_p()
+        check(self.lib.dmx_create(index, ctypes.byref(h)))
+        self.handle = h
+        self.tmax = 0
+
+    @classmethod
+    def get(cls, device: torch.device) -> "Context":
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        with cls._lock:
+            if idx not in cls._ctxs:
+                cls._ctxs[idx] = Context(idx)
+            return cls._ctxs[idx]
+
+    def ensure_time_table(self, tmax: int) -> None:
+        if tmax <= self.tmax:
+            return
+        tmax = max(tmax, 1000)
+        tab = pos_table(tmax)
+        check(self.lib.dmx_set_time_table(self.handle, ctypes.c_void_p(tab.data_ptr()), tmax))
+        self.tmax = tmax
+
+
+def require_cuda(t: torch.Tensor, what: str) -> None:
+    if not t.is_cuda:
+        raise _lib.DmxUnavailable(
+            f"{what} is on {t.device}; the dmx path runs only on an MI355X (HIP) device — move the model and "
+            f"inputs with .to('cuda') (there is no CPU fallback)")
+
+
+class NativeModel:
+    """A repacked copy of one reference network inside libdmx (U-Net or VAE)."""
+
+    def __init__(self, kind: int, params: Dict[str, torch.Tensor], in_ch: int = 4, remove_deep_conv: bool = False):
+        self.kind = kind
+        self.in_ch = in_ch
+        some = next(iter(params.values()))
+        require_cuda(some, "model weights")
+        self.device = some.device
+        self.ctx = Context.get(self.device)
+        self.lib = self.ctx.lib
+        h = ctypes.c_void_p()
+        check(self.lib.dmx_model_create(self.ctx.handle, kind, in_ch, int(remove_deep_conv), ctypes.byref(h)))
+        self.handle = h
+        keep = []
+        for name, t in params.items():
+            tt = t.detach().to(dtype=torch.float32).contiguous()
+            keep.append(tt)
+            shape = (ctypes.c_int64 * max(tt.dim(), 1))(*tt.shape)
+            check(self.lib.dmx_model_set_tensor(self.handle, name.encode(), ctypes.c_void_p(tt.data_ptr()), shape,
+                                                tt.dim()))
+        with torch.cuda.device(self.device):
+            check(self.lib.dmx_model_finalize(self.handle, ctypes.c_void_p(_stream(self.device))))
+        del keep
+        self._side_stream = None
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None):
+                self.lib.dmx_model_destroy(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+    def workspace_bytes(self) -> int:
+        return int(self.lib.dmx_model_workspace_bytes(self.handle))
+
+    # ---- U-Net ---------------------------------------------------------------------------
+    def forward(self, x, t, y=None, vals=None, mask=None, want_geom=False):
+        n, c, h, w = x.shape
+        self.ctx.ensure_time_table(int(t.max().item()) if t.numel() else 1)
+        x = x.contiguous().float()
+        t = t.to(device=x.device, dtype=torch.long).contiguous()
+        if y is not None:
+            y = y.to(device=x.device, dtype=torch.long).contiguous()
+        if vals is not None:
+            vals = vals.to(device=x.device, dtype=torch.float32).contiguous()
+            mask = mask.to(device=x.device, dtype=torch.float32).contiguous()
+        eps = torch.empty_like(x)
+        geom = torch.empty((n, 12), device=x.device, dtype=torch.float32) if want_geom else None
+        with torch.cuda.device(x.device):
+            check(self.lib.dmx_unet_forward(self.handle, _ptr(x), _ptr(t), _ptr(y), _ptr(vals), _ptr(mask),
+                                            _ptr(eps), _ptr(geom), n, h, w, ctypes.c_void_p(_stream(x.device))))
+        return eps, geom
+
+    def forward_taps(self, x, t, y=None, vals=None, mask=None):
+        """Forward with debug taps -> {name: flat float32 tensor (NHWC order)}."""
+        check(self.lib.dmx_debug_enable(self.handle, 1))
+        try:
+            eps, geom = self.forward(x, t, y, vals, mask, want_geom=self.kind == _lib.DMX_UNET_COND_GEOM)
+            out = {}
+            buf = ctypes.create_string_buffer(128)
+            cnt = ctypes.c_int64()
+            for i in range(self.lib.dmx_debug_num_taps(self.handle)):
+                check(self.lib.dmx_debug_tap(self.handle, i, buf, 128, ctypes.byref(cnt), None, None))
+                dst = torch.empty(cnt.value, device=x.device, dtype=torch.float32)
+                check(self.lib.dmx_debug_tap(self.handle, i, buf, 128, ctypes.byref(cnt), _ptr(dst),
+                                             ctypes.c_void_p(_stream(x.device))))
+                out[buf.value.decode()] = dst
+            torch.cuda.synchronize(x.device)
+            out["eps"] = eps
+            return out
+        finally:
+            check(self.lib.dmx_debug_enable(self.handle, 0))
+
+    def _args(self, x_in, x_out, t, t_stride, y, null_label, vals, mask, guidance, tables, noise, seed,
+              sample_offset) -> StepArgs:
+        c1, c2, sd = tables
+        n, _, h, w = x_in.shape
+        a = StepArgs()
+        a.x_in, a.x_out = x_in.data_ptr(), x_out.data_ptr()
+        a.t, a.t_stride = t.data_ptr(), t_stride
+        a.y = y.data_ptr() if y is not None else None
+        a.null_label = int(null_label)
+        a.vals = vals.data_ptr() if vals is not None else None
+        a.mask = mask.data_ptr() if mask is not None else None
+        a.guidance = float(guidance)
+        a.c1, a.c2, a.sd, a.T = c1.data_ptr(), c2.data_ptr(), sd.data_ptr(), int(c1.numel())
+        a.noise = noise.data_ptr() if noise is not None else None
+        a.seed, a.sample_offset = int(seed) & 0xFFFFFFFFFFFFFFFF, int(sample_offset)
+        a.n, a.h, a.w = n, h, w
+        return a
+
+    def step(self, x_in, x_out, t, y, null_label, vals, mask, guidance, tables, noise=None, seed=0,
+             sample_offset=0, t_stride=1):
+        """One denoising step: CFG (2n batched forward) when guidance > 0 and y given."""
+        self.ctx.ensure_time_table(int(tables[0].numel()))
+        a = self._args(x_in, x_out, t, t_stride, y, null_label, vals, mask, guidance, tables, noise, seed,
+                       sample_offset)
+        with torch.cuda.device(x_in.device):
+            check(self.lib.dmx_step(self.handle, ctypes.byref(a), ctypes.c_void_p(_stream(x_in.device))))
+
+    def step_profile(self, x_in, x_out, t, y, null_label, vals, mask, guidance, tables, noise=None, seed=0,
+                     t_stride=1, cap=1024):
+        """One eager step with event timing per launch -> list of dicts."""
+        self.ctx.ensure_time_table(int(tables[0].numel()))
+        a = self._args(x_in, x_out, t, t_stride, y, null_label, vals, mask, guidance, tables, noise, seed, 0)
+        recs = (_lib.KernelRecord * cap)()
+        n = ctypes.c_int()
+        with torch.cuda.device(x_in.device):
+            check(self.lib.dmx_step_profile(self.handle, ctypes.byref(a), recs, cap, ctypes.byref(n),
+                                            ctypes.c_void_p(_stream(x_in.device))))
+        return [dict(kernel=r.kernel.decode(), layer=r.layer.decode(), flops=r.flops, bytes=r.bytes, ms=r.ms)
+                for r in recs[:n.value]]
+
+    def side_stream(self) -> torch.cuda.Stream:
+        if self._side_stream is None:
+            self._side_stream = torch.cuda.Stream(self.device)
+        return self._side_stream
+
+    def sample_loop(self, x, t_dev, y, null_label, vals, mask, guidance, tables, steps, seed=0, sample_offset=0,
+                    use_graph=True):
+        """`steps` in-place steps on x with Philox noise; t_dev (device int64 scalar) is
+        decremented on the device after each step.  Runs on a side stream (graph capture
+        needs a non-default stream) ordered against the current stream."""
+        self.ctx.ensure_time_table(int(tables[0].numel()))
+        a = self._args(x, x, t_dev, 0, y, null_label, vals, mask, guidance, tables, None, seed, sample_offset)
+        cur = torch.cuda.current_stream(x.device)
+        side = self.side_stream()
+        side.wait_stream(cur)
+        with torch.cuda.device(x.device):
+            check(self.lib.dmx_sample_loop(self.handle, ctypes.byref(a), int(steps), int(use_graph),
+                                           ctypes.c_void_p(side.cuda_stream)))
+        cur.wait_stream(side)
+
+    # ---- VAE -----------------------------------------------------------------------------
+    def decode(self, z, want_img=True, want_u8=False) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
+        n, c, h, w = z.shape
+        z = z.contiguous().float()
+        img = torch.empty((n, 3, 8 * h, 8 * w), device=z.device, dtype=torch.float32) if want_img else None
+        u8 = torch.empty((n, 8 * h, 8 * w, 3), device=z.device, dtype=torch.uint8) if want_u8 else None
+        with torch.cuda.device(z.device):
+            check(self.lib.dmx_vae_decode(self.handle, _ptr(z), _ptr(img), _ptr(u8), n, h, w,
+                                          ctypes.c_void_p(_stream(z.device))))
+        return img, u8
+
+
+def ddpm_update(x, eu, ec, guidance, t, tables, noise=None, seed=0, sample_offset=0):
+    """Standalone K1 (diff.py:151,158-162) for duck-typed models: returns x'."""
+    lib = _lib.load()
+    c1, c2, sd = tables
+    n, c, h, w = x.shape
+    out = torch.empty_like(x)
+    t = t.to(device=x.device, dtype=torch.long).contiguous()
+    with torch.cuda.device(x.device):
+        check(lib.dmx_ddpm_update(_ptr(x.contiguous()), _ptr(out), _ptr(eu.contiguous().float()),
+                                  _ptr(ec.contiguous().float() if ec is not None else None), float(guidance), _ptr(t),
+                                  1, _ptr(c1), _ptr(c2), _ptr(sd), int(c1.numel()),
+                                  _ptr(noise.contiguous() if noise is not None else None), int(seed),
+                                  int(sample_offset), n, c, h, w, ctypes.c_void_p(_stream(x.device))))
+    return out

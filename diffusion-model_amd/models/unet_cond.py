@@ -1,0 +1,46 @@
+"""Drop-in ``models.unet_cond`` (reference models/unet_cond.py:102-216).
+
+``UnetCond`` keeps the reference constructor, attributes and state_dict keys;
+its forward runs the native U-Net of libdmx (conv3x3+GroupNorm+GELU residual
+blocks, 4-head self-attention at six resolutions, sinusoidal time + class +
+geometric-condition embedding) and returns eps like the reference.
+"""
+from __future__ import annotations
+
+import torch
+
+from dmx import _lib, spec
+from models._native import NativeBacked, build_param_tree
+
+
+class UnetCond(NativeBacked):
+    """Conditional latent U-Net (reference models/unet_cond.py:102-153)."""
+
+    _dmx_kind = _lib.DMX_UNET_COND
+
+    def __init__(self, in_ch=4, time_dim=256, num_classes=3, cfg_drop_prob=0.1, remove_deep_conv=False):
+        super().__init__()
+        if time_dim != 256 or num_classes != 3:
+            raise ValueError("dmx implements the reference configuration time_dim=256, num_classes=3")
+        self.time_dim = time_dim
+        self.remove_deep_conv = remove_deep_conv
+        self.num_classes = num_classes
+        self.cfg_drop_prob = cfg_drop_prob
+        self._dmx_in_ch = in_ch
+        build_param_tree(self, self._spec(in_ch, remove_deep_conv))
+
+    def _spec(self, in_ch, remove_deep_conv):
+        return spec.unet_cond_spec(in_ch=in_ch, remove_deep_conv=remove_deep_conv)
+
+    def _check_training(self, cond_drop_prob=None):
+        p = self.cfg_drop_prob if cond_drop_prob is None else cond_drop_prob
+        if self.training and (self.cfg_drop_prob > 0 or (p or 0) > 0) and type(self) is UnetCond:
+            # models/unet_cond.py:199-211: random CFG label/cond dropout is a training-time feature
+            raise NotImplementedError("training-mode CFG dropout is out of scope for dmx; call .eval()")
+
+    def forward(self, x: torch.Tensor, t: torch.Tensor, y: torch.Tensor, cond_vals: torch.Tensor = None,
+                cond_mask: torch.Tensor = None, cond_drop_prob: float = None):
+        self._check_training(cond_drop_prob)
+        use = cond_vals is not None and cond_mask is not None  # models/unet_cond.py:205
+        eps, _ = self.native().forward(x, t, y, cond_vals if use else None, cond_mask if use else None)
+        return eps

@@ -1,0 +1,291 @@
+"""HIP path vs the oracle / the reference's golden vectors (MI355X only).
+
+Tolerances (fp32 everywhere):
+  * single network forwards / single steps: rel-L2 <= 2e-5 (different but fp32-exact
+    accumulation orders; measured ~1e-6)
+  * latents after a full T=1000 CFG trajectory: rel-L2 <= 1e-4 (north-star bound)
+  * decoded uint8 pixels: |diff| <= 1 LSB on <= 0.1% of values (truncating quantiser)
+  * the DDPM/CFG update itself (given eps): bit-exact
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref
+
+pytestmark = pytest.mark.gpu
+
+TOL = 2e-5
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).double().cpu()
+    b = torch.as_tensor(b).double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def u8_close(a, b, frac=1e-3):
+    d = np.abs(np.asarray(a, np.int32) - np.asarray(b, np.int32))
+    return d.max() <= 1 and (d > 0).mean() <= frac, (int(d.max()), float((d > 0).mean()))
+
+
+@pytest.fixture(scope="module")
+def model(cuda, unet_sd):
+    from models.unet_cond_geom import UnetCondWithGeomHead
+    m = UnetCondWithGeomHead()
+    m.load_state_dict(unet_sd)
+    return m.to(cuda).eval()
+
+
+@pytest.fixture(scope="module")
+def vae(cuda, vae_sd):
+    from models.vae import VAE
+    v = VAE()
+    v.load_state_dict(vae_sd)
+    return v.to(cuda).eval()
+
+
+def test_library_is_native(cuda):
+    import ctypes
+    from dmx import _lib
+    lib = _lib.load()
+    assert lib.dmx_abi_version() == 1
+    assert isinstance(lib, ctypes.CDLL)
+
+
+@pytest.mark.parametrize("name", ["forward_32.npz", "forward_28.npz"])
+def test_unet_forward_golden(golden, model, cuda, name):
+    g = golden(name)
+    dev = lambda k: torch.from_numpy(g[k]).to(cuda)
+    with torch.no_grad():
+        eps, geom = model(dev("x"), dev("t"), dev("y"), cond_vals=dev("vals"), cond_mask=dev("mask"))
+    assert rel(eps, g["eps"]) < TOL
+    assert rel(geom, g["geom"]) < TOL
+
+
+def test_unet_forward_vs_oracle_no_cond(model, cuda, unet_sd):
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn((5, 4, 32, 32), generator=g)
+    t = torch.tensor([1, 2, 500, 999, 1000])
+    y = torch.tensor([0, 1, 2, 3, 1])
+    with torch.no_grad():
+        eps, geom = model(x.to(cuda), t.to(cuda), y.to(cuda))
+        e2, g2 = ref.unet_cond_geom_forward(unet_sd, x, t, y)
+    assert rel(eps, e2) < TOL and rel(geom, g2) < TOL
+
+
+def test_uncond_unet_golden(golden, cuda):
+    from dmx import synth
+    from models.unet import Unet
+    m = Unet(in_ch=4)
+    m.load_state_dict(synth.unet_weights(0, in_ch=4))
+    m.to(cuda).eval()
+    g = golden("forward_uncond.npz")
+    with torch.no_grad():
+        eps = m(torch.from_numpy(g["x"]).to(cuda), torch.from_numpy(g["t"]).to(cuda))
+    assert rel(eps, g["eps"]) < TOL
+
+
+def test_vae_decode_golden(golden, vae, cuda):
+    g = golden("vae_decode.npz")
+    with torch.no_grad():
+        img16 = vae.decode(torch.from_numpy(g["z16"]).to(cuda))
+        u8 = vae.decode_uint8(torch.from_numpy(g["z32"]).to(cuda))
+    assert rel(img16, g["img16"]) < TOL
+    ok, info = u8_close(u8.cpu().numpy(), g["u8_32"])
+    assert ok, info
+
+
+def test_vae_decode_vs_oracle_odd_batch(vae, cuda, vae_sd):
+    z = torch.randn((3, 4, 8, 8), generator=torch.Generator().manual_seed(4))
+    with torch.no_grad():
+        img = vae.decode(z.to(cuda))
+        exp = ref.vae_decode(vae_sd, z)
+    assert rel(img, exp) < TOL
+
+
+def test_denoise_cond_golden_steps(golden, model, cuda):
+    import diff
+    g = golden("denoise_cond.npz")
+    d = diff.Diffuser(1000, device=cuda)
+    x = torch.from_numpy(g["x"]).to(cuda)
+    y = torch.from_numpy(g["y"]).to(cuda)
+    vals, mask = torch.from_numpy(g["vals"]).to(cuda), torch.from_numpy(g["mask"]).to(cuda)
+    for tv in (1000, 500, 2, 1):
+        t = torch.full((2,), tv, dtype=torch.long, device=cuda)
+        torch.manual_seed(100 + tv)  # same global-generator draw as the reference
+        out = d.denoise_cond(model, x, t, y=y, guidance_scale=3.0, null_label=0, cond_vals=vals, cond_mask=mask)
+        assert rel(out, g[f"out_{tv}"]) < TOL, tv
+
+
+def test_ddpm_update_bit_exact(cuda):
+    """K1 given eps: one rounding per reference op, same order => bit-identical to torch-CPU."""
+    import diff
+    from dmx import engine
+    d = diff.Diffuser(1000, device=cuda)
+    g = torch.Generator().manual_seed(9)
+    B = 6
+    x, eu, ec, nz = (torch.randn((B, 4, 16, 16), generator=g) for _ in range(4))
+    t = torch.tensor([1, 2, 3, 500, 999, 1000])
+    out = engine.ddpm_update(x.to(cuda), eu.to(cuda), ec.to(cuda), 3.0, t.to(cuda),
+                             d.coef_tables(cuda, True), nz.to(cuda)).cpu()
+    _, a, ab = ref.schedule(1000)
+    eps = eu + 3.0 * (ec - eu)
+    exp = ref.ddpm_update(x, eps, t, a, ab, nz)
+    assert torch.equal(out, exp)
+    # unconditional variant (diff.py:39 wrap-around alpha_bar_prev)
+    out2 = engine.ddpm_update(x.to(cuda), eu.to(cuda), None, 0.0, t.to(cuda), d.coef_tables(cuda, False),
+                              nz.to(cuda)).cpu()
+    assert torch.equal(out2, ref.ddpm_update(x, eu, t, a, ab, nz, clamp_prev=False))
+
+
+def test_cfg_step_full_batch_vs_oracle(model, cuda, unet_sd):
+    """One CFG step at the benchmark shape B=64, 32x32x4 (2B = 128 sample-forwards)."""
+    import diff
+    d = diff.Diffuser(1000, device=cuda)
+    g = torch.Generator().manual_seed(21)
+    B = 64
+    x = torch.randn((B, 4, 32, 32), generator=g)
+    y = torch.tensor([1 + i % 3 for i in range(B)])
+    vals = torch.rand((B, 12), generator=g)
+    mask = (torch.rand((B, 12), generator=g) > 0.5).float()
+    t = torch.full((B,), 640, dtype=torch.long)
+    torch.manual_seed(77)
+    out = d.denoise_cond(model, x.to(cuda), t.to(cuda), y=y.to(cuda), guidance_scale=3.0,
+                         cond_vals=vals.to(cuda), cond_mask=mask.to(cuda))
+    torch.manual_seed(77)
+    noise = torch.randn(x.shape)
+    _, a, ab = ref.schedule(1000)
+    with torch.no_grad():
+        exp = ref.cfg_step(unet_sd, x, t, y, a, ab, 3.0, 0, vals, mask, noise)
+    assert rel(out, exp) < TOL
+
+
+def test_trajectory_T1000_golden(golden, model, vae, cuda):
+    """Full T=1000 CFG trajectory (B=2) on the reference's own draws: latents <= 1e-4, pixels +-1."""
+    import diff
+    g = golden("traj_T1000_B2.npz")
+    d = diff.Diffuser(1000, device=cuda)
+    y = torch.from_numpy(g["y"]).to(cuda)
+    vals, mask = torch.from_numpy(g["vals"]).to(cuda), torch.from_numpy(g["mask"]).to(cuda)
+    torch.manual_seed(int(g["seed"]))
+    x = torch.randn((2, 4, 32, 32)).to(cuda)
+    for i in range(1000, 0, -1):
+        t = torch.full((2,), i, dtype=torch.long, device=cuda)
+        x = d.denoise_cond(model, x, t, y=y, guidance_scale=3.0, null_label=0, cond_vals=vals, cond_mask=mask)
+        if i in (900, 500, 100):
+            assert rel(x, g[f"x_{i}"]) < 1e-4, i
+    assert rel(x, g["x_final"]) < 1e-4
+    u8 = vae.decode_uint8(x).cpu().numpy()
+    ok, info = u8_close(u8, g["u8"])
+    assert ok, info
+
+
+def test_sample_latent_cond_T20_28_path(golden, model, vae, cuda):
+    """z_shape=None (28x28 latents via the replayed encode draw), pixels via PIL, and z_shape given."""
+    import diff
+    g = golden("sample_T20.npz")
+    d = diff.Diffuser(20, device=cuda)
+    torch.manual_seed(int(g["seed"]))
+    imgs = d.sample_latent_cond(model, (2, 2), vae=vae, to_pil=True, progress=False, guidance_scale=3.0,
+                                cond=torch.from_numpy(g["vals"]).to(cuda), cond_mask=torch.from_numpy(g["mask"]).to(cuda))
+    u8 = np.stack([np.asarray(im) for im in imgs])
+    ok, info = u8_close(u8, g["u8_28"])
+    assert ok, info
+    torch.manual_seed(int(g["seed"]))
+    lat = d.sample_latent_cond(model, {1: 1, 3: 1}, z_shape=(4, 32, 32), vae=None, progress=False)
+    assert rel(lat, g["latent_32"]) < 1e-4
+
+
+def test_uncond_sample_latent_T100_golden(golden, cuda):
+    """Config 1: unconditional Unet, T=100, B=4 (diff.py:87-125)."""
+    import diff
+    from dmx import synth
+    from models.unet import Unet
+    m = Unet(in_ch=4)
+    m.load_state_dict(synth.unet_weights(0, in_ch=4))
+    m.to(cuda).eval()
+    g = golden("uncond_T100.npz")
+    d = diff.Diffuser(100, device=cuda)
+    torch.manual_seed(int(g["seed"]))
+    z = d.sample_latent(m, z_shape=(4, 4, 32, 32), vae=None, progress=False)
+    assert rel(z, g["latent"]) < 1e-4
+
+
+def test_graph_loop_equals_eager_and_is_deterministic(model, cuda):
+    """Device-noise mode: hipGraph replay == eager launches, bit for bit, and reruns are identical."""
+    from dmx import engine  # noqa: F401
+    import diff
+    d = diff.Diffuser(1000, device=cuda)
+    nm = model.native()
+    B = 4
+    g = torch.Generator().manual_seed(2)
+    x0 = torch.randn((B, 4, 32, 32), generator=g).to(cuda)
+    y = torch.tensor([1, 2, 3, 1], device=cuda)
+    vals = torch.rand((B, 12), generator=g).to(cuda)
+    mask = torch.ones((B, 12), device=cuda)
+    tables = d.coef_tables(cuda, True)
+    outs = []
+    for use_graph in (True, False, True):
+        x = x0.clone()
+        t = torch.full((1,), 1000, dtype=torch.long, device=cuda)
+        nm.sample_loop(x, t, y, 0, vals, mask, 3.0, tables, 7, seed=1234, use_graph=use_graph)
+        torch.cuda.synchronize()
+        assert int(t.item()) == 993
+        outs.append(x.cpu())
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert torch.isfinite(outs[0]).all()
+
+
+def test_philox_noise_statistics_and_shard_invariance(model, cuda):
+    """Perf-mode noise: N(0,1) moments, and sample i's noise does not depend on the shard it runs in."""
+    from dmx import engine
+    import diff
+    d = diff.Diffuser(1000, device=cuda)
+    B = 8
+    x = torch.zeros((B, 4, 32, 32), device=cuda)
+    eu = torch.zeros_like(x)
+    t = torch.full((B,), 2, dtype=torch.long, device=cuda)
+    tab = d.coef_tables(cuda, True)
+    full = engine.ddpm_update(x, eu, None, 0.0, t, tab, None, seed=99, sample_offset=0)
+    part = engine.ddpm_update(x[4:], eu[4:], None, 0.0, t[4:], tab, None, seed=99, sample_offset=4)
+    assert torch.equal(full[4:], part)
+    z = (full / tab[2][1]).flatten().double()
+    assert abs(float(z.mean())) < 0.02 and abs(float(z.std()) - 1.0) < 0.02
+
+
+def test_edge_cases_batch1_per_sample_t_nonzero_null(model, cuda, unet_sd):
+    import diff
+    d = diff.Diffuser(1000, device=cuda)
+    for B, tv, null in ((1, [1], 0), (3, [1, 500, 1000], 2)):
+        g = torch.Generator().manual_seed(B)
+        x = torch.randn((B, 4, 32, 32), generator=g)
+        y = torch.tensor([3, 1, 2][:B])
+        vals = torch.rand((B, 12), generator=g)
+        mask = torch.ones((B, 12))
+        t = torch.tensor(tv)
+        torch.manual_seed(11)
+        out = d.denoise_cond(model, x.to(cuda), t.to(cuda), y=y.to(cuda), guidance_scale=2.5, null_label=null,
+                             cond_vals=vals.to(cuda), cond_mask=mask.to(cuda))
+        torch.manual_seed(11)
+        _, a, ab = ref.schedule(1000)
+        with torch.no_grad():
+            exp = ref.cfg_step(unet_sd, x, t, y, a, ab, 2.5, null, vals, mask, torch.randn(x.shape))
+        assert rel(out, exp) < TOL, B
+
+
+def test_reference_error_behaviour(model, cuda):
+    import diff
+    d = diff.Diffuser(1000, device=cuda)
+    x = torch.zeros((1, 4, 32, 32), device=cuda)
+    y = torch.ones((1,), dtype=torch.long, device=cuda)
+    with pytest.raises(AssertionError):
+        d.denoise_cond(model, x, torch.tensor([0], device=cuda), y=y, guidance_scale=3.0)
+    with pytest.raises(AssertionError):
+        d.denoise_cond(model, x, torch.tensor([1001], device=cuda), y=y, guidance_scale=3.0)
+    with pytest.raises(UnboundLocalError):  # diff.py:152-156 with y given and guidance 0
+        d.denoise_cond(model, x, torch.tensor([5], device=cuda), y=y, guidance_scale=0.0)
+    with pytest.raises(TypeError):  # y=None: eps is the (eps, geom) tuple of the geom model
+        d.denoise_cond(model, x, torch.tensor([5], device=cuda), y=None, guidance_scale=0.0)
+    with pytest.raises(ValueError):
+        d.sample_latent_cond(model, {1: 0}, z_shape=(4, 32, 32))

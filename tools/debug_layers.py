@@ -1,0 +1,110 @@
+"""Layer-by-layer comparison of the native U-Net forward against the oracle (GPU box).
+
+  python tools/debug_layers.py [--hw 32] [--n 3]
+Prints rel-L2 of every tapped block output (NHWC) vs the oracle's intermediate.
+"""
+import argparse
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "diffusion-model_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from dmx import synth  # noqa: E402
+from oracle import ref  # noqa: E402
+
+
+def nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous().flatten() if t.dim() == 4 else t.flatten()
+
+
+def oracle_taps(sd, x, t, y, vals, mask):
+    T = {}
+    emb = ref.cond_embedding(sd, t, y, vals, mask)
+    heads = [F.linear(F.silu(emb), sd[f"{b}.emb_layer.1.weight"], sd[f"{b}.emb_layer.1.bias"])
+             for b in ("down1", "down2", "down3", "up1", "up2", "up3")]
+    T["emb"] = torch.cat(heads, dim=1).flatten()
+
+    def res(name, p, h, residual):
+        T[name + ".r1"] = nhwc(F.conv2d(h, sd[f"{p}.double_conv.0.weight"], None, 1, 1))
+        o = ref.resblock(sd, p, h, residual)
+        T[name] = nhwc(o)
+        return o
+
+    def attn(name, h):
+        n, c, hh, ww = h.shape
+        tok = h.reshape(n, c, hh * ww).transpose(1, 2)
+        xl = F.layer_norm(tok, (c,), sd[f"{name}.ln.weight"], sd[f"{name}.ln.bias"], 1e-5)
+        T[name + ".xl"] = xl.flatten()
+        T[name + ".qkv"] = F.linear(xl, sd[f"{name}.mha.in_proj_weight"], sd[f"{name}.mha.in_proj_bias"]).flatten()
+        o = ref.attention(sd, name, h)
+        T[name] = nhwc(o)
+        return o
+
+    x1 = res("inc", "inc", x, False)
+    cur = x1
+    skips = []
+    for i in range(3):
+        skips.append(cur)
+        d = f"down{i + 1}"
+        h0 = res(d + ".0", d + ".maxpool_conv.1", F.max_pool2d(cur, 2), True)
+        h1 = ref.resblock(sd, d + ".maxpool_conv.2", h0, False) + ref.emb_head(sd, d, emb)
+        T[d + ".1"] = nhwc(h1)
+        cur = attn(f"sa{i + 1}", h1)
+    for i, b in enumerate(("bot1", "bot2", "bot3")):
+        cur = res(f"bot{i + 1}", b, cur, False)
+    for i in range(3):
+        u = f"up{i + 1}"
+        skip = skips[2 - i]
+        h = F.interpolate(cur, scale_factor=2, mode="bilinear", align_corners=True)
+        dy, dx = skip.size(2) - h.size(2), skip.size(3) - h.size(3)
+        if dy or dx:
+            h = F.pad(h, [max(0, dx // 2), max(0, dx - dx // 2), max(0, dy // 2), max(0, dy - dy // 2)])
+        h = torch.cat([skip, h], 1)
+        h0 = res(u + ".0", u + ".conv.0", h, True)
+        h1 = ref.resblock(sd, u + ".conv.1", h0, False) + ref.emb_head(sd, u, emb)
+        T[u + ".1"] = nhwc(h1)
+        cur = attn(f"sa{4 + i}", h1)
+    T["eps"] = F.conv2d(cur, sd["out.weight"], sd["out.bias"]).flatten()
+    return T
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--hw", type=int, default=32)
+    ap.add_argument("--n", type=int, default=3)
+    a = ap.parse_args()
+    from models.unet_cond_geom import UnetCondWithGeomHead
+    sd = synth.unet_cond_geom_weights(0)
+    m = UnetCondWithGeomHead()
+    m.load_state_dict(sd)
+    dev = torch.device("cuda:0")
+    m.to(dev).eval()
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn((a.n, 4, a.hw, a.hw), generator=g)
+    t = torch.tensor([1000, 517, 1, 42, 7][: a.n])
+    y = torch.tensor([0, 2, 3, 1, 1][: a.n])
+    vals = torch.rand((a.n, 12), generator=g)
+    mask = (torch.rand((a.n, 12), generator=g) > 0.5).float()
+    with torch.no_grad():
+        nat = m.native().forward_taps(x.to(dev), t.to(dev), y.to(dev), vals.to(dev), mask.to(dev))
+        ora = oracle_taps(sd, x, t, y, vals, mask)
+    for k, v in nat.items():
+        v = v.flatten().double().cpu()
+        if k not in ora:
+            print(f"{k:14s} (no oracle)  norm={float(v.norm()):.4e}")
+            continue
+        o = ora[k].double()
+        if o.numel() != v.numel():
+            print(f"{k:14s} SIZE MISMATCH native {v.numel()} oracle {o.numel()}")
+            continue
+        r = float((v - o).norm() / o.norm().clamp_min(1e-30))
+        print(f"{k:14s} rel={r:.3e}  maxabs={float((v - o).abs().max()):.3e}  norm={float(o.norm()):.4e}")
+
+
+if __name__ == "__main__":
+    main()
