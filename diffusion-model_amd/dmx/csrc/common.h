@@ -33,6 +33,7 @@ enum EpiMode : int {
   EPI_BIAS = 1,      // acc + bias
   EPI_BIAS_GELU = 2, // GELU(acc + bias)
   EPI_BIAS_RES = 3,  // acc + bias + res
+  EPI_PARTIAL = 4,   // split-K: raw accumulator into slab[split] (epilogue in splitk_reduce)
 };
 
 struct SrcDesc {

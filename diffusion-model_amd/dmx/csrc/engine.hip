@@ -510,16 +510,35 @@ static void launch_ig_tiles(int bm, int bn, const IgemmParams& p, dim3 grid, hip
   else launch_ig<64, 64, SRC, EPI>(p, grid, st);
 }
 
-// Implicit GEMM: conv3x3 (taps 9), ConvT phases (taps 4, phases 4), linear (taps 1)
-static void gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, const ConvW& cw, int epi, float* out,
-                 const float* res, float2* rowpart, int seg) {
-  if (R.plan) return;
+// Implicit GEMM: conv3x3 (taps 9), ConvT phases (taps 4, phases 4), linear (taps 1).
+// Sources are plain NHWC (or the NCHW network input); grids too small to fill the
+// 256 CUs are split along K into deterministic slabs reduced by splitk_reduce_kernel.
+// Returns the GroupNorm partial rows per sample it wrote (EPI_STATS).
+static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, const ConvW& cw, int epi, float* out,
+                const float* res, float2* rowpart, int seg) {
+  const int M = N * H * W;
+  if (cw.cout % 32 != 0) throw Error(DMX_E_INTERNAL, "gemm: Cout must be a multiple of 32");
+  const int bn = (cw.cout % 128 == 0) ? 128 : 64;
+  const int tiles128 = cdiv(M, 128) * cdiv(cw.cout, bn) * cw.phases;
+  const int bm = tiles128 >= 512 ? 128 : 64;
+  const int blocks = cdiv(M, bm) * cdiv(cw.cout, bn) * cw.phases;
+  const int nkt = cw.kpad / IG_BK;
+  int splits = 1, ksplit = nkt;
+  if (cw.phases == 1 && blocks < 256 && nkt >= 32) {
+    splits = std::min(std::min(8, std::max(2, 512 / blocks)), nkt / 16);
+    ksplit = cdiv(nkt, splits);
+    splits = cdiv(nkt, ksplit);
+  }
+  float* partial = splits > 1 ? R.ws.get<float>((size_t)splits * M * cw.cout) : nullptr;
+  const int rgrp = (splits == 1 && (H * W) % 32 == 0) ? 32 : 1;
+  const int rrows = cw.phases * H * W / rgrp;
+  if (R.plan) return rrows;
   IgemmParams p;
   std::memset(&p, 0, sizeof(p));
   p.src = s;
   p.H = H;
   p.W = W;
-  p.M = N * H * W;
+  p.M = M;
   p.taps = cw.taps;
   for (int ph = 0; ph < cw.phases; ++ph) {
     for (int t = 0; t < cw.taps; ++t) {
@@ -548,32 +567,41 @@ static void gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, co
   p.res = res;
   p.rowpart = rowpart;
   p.seg = seg;
+  p.ksplit = ksplit;
+  p.partial = partial;
+  p.rgrp = rgrp;
+  p.nphase = cw.phases;
   if (s.C != cw.cin) throw Error(DMX_E_INTERNAL, "gemm: source channels != weight channels");
-  if (cw.cout % 32 != 0) throw Error(DMX_E_INTERNAL, "gemm: Cout must be a multiple of 32");
-  const int bn = (cw.cout % 128 == 0) ? 128 : 64;
-  const int tiles128 = cdiv(p.M, 128) * cdiv(cw.cout, bn) * cw.phases;
-  const int bm = tiles128 >= 512 ? 128 : 64;
-  dim3 grid(cdiv(p.M, bm), cdiv(cw.cout, bn), cw.phases);
-  {
-    const int creal = (src_mode == SRC_NCHW && s.C0) ? s.C0 : cw.cin;
-    const double flops = 2.0 * (double)p.M * cw.phases * cw.cout * (double)cw.taps * creal;
-    const double bytes = 4.0 * ((double)p.M * cw.phases * cw.cout + (double)p.M * s.C +
-                                (double)cw.phases * cw.cout * cw.taps * cw.cin);
-    char nm[96];
-    std::snprintf(nm, sizeof nm, "igemm_f32_kernel<%d, %d, %d, %d>", bm, bn, epi == EPI_STATS ? src_mode : SRC_PLAIN,
-                  epi);
-    R.begin(nm, flops, bytes);
+  if (src_mode != SRC_PLAIN && src_mode != SRC_NCHW) throw Error(DMX_E_INTERNAL, "gemm: unsupported source");
+  const int creal = (src_mode == SRC_NCHW && s.C0) ? s.C0 : cw.cin;
+  const double flops = 2.0 * (double)M * cw.phases * cw.cout * (double)cw.taps * creal;
+  const double bytes = 4.0 * ((double)M * cw.phases * cw.cout + (double)M * s.C +
+                              (double)cw.phases * cw.cout * cw.taps * cw.cin);
+  char nm[96];
+  if (splits > 1) {
+    dim3 grid(cdiv(M, bm), cdiv(cw.cout, bn), splits);
+    std::snprintf(nm, sizeof nm, "igemm_f32_kernel<%d, %d, %d, %d>", bm, bn, src_mode, (int)EPI_PARTIAL);
+    R.begin(nm, flops, bytes + 4.0 * splits * M * cw.cout);
+    if (src_mode == SRC_NCHW) launch_ig_tiles<SRC_NCHW, EPI_PARTIAL>(bm, bn, p, grid, R.st);
+    else launch_ig_tiles<SRC_PLAIN, EPI_PARTIAL>(bm, bn, p, grid, R.st);
+    R.end();
+    HIPCHK(hipGetLastError());
+    SplitkParams q{partial, splits, M, cw.cout, cw.bias, res, out, rowpart, seg, epi};
+    const int rb = cdiv(M * (cw.cout / 4), 256);
+    R.begin("splitk_reduce_kernel", 0.0, 4.0 * (double)(splits + 1) * M * cw.cout);
+    splitk_reduce_kernel<<<rb, 256, 0, R.st>>>(q);
+    R.end();
+    HIPCHK(hipGetLastError());
+    return rrows;
   }
+  dim3 grid(cdiv(M, bm), cdiv(cw.cout, bn), cw.phases);
+  std::snprintf(nm, sizeof nm, "igemm_f32_kernel<%d, %d, %d, %d>", bm, bn, epi == EPI_STATS ? src_mode : SRC_PLAIN,
+                epi);
+  R.begin(nm, flops, bytes);
   switch (epi) {
     case EPI_STATS:
-      switch (src_mode) {
-        case SRC_PLAIN: launch_ig_tiles<SRC_PLAIN, EPI_STATS>(bm, bn, p, grid, R.st); break;
-        case SRC_GNACT: launch_ig_tiles<SRC_GNACT, EPI_STATS>(bm, bn, p, grid, R.st); break;
-        case SRC_MAXPOOL: launch_ig_tiles<SRC_MAXPOOL, EPI_STATS>(bm, bn, p, grid, R.st); break;
-        case SRC_UPCAT: launch_ig_tiles<SRC_UPCAT, EPI_STATS>(bm, bn, p, grid, R.st); break;
-        case SRC_NCHW: launch_ig_tiles<SRC_NCHW, EPI_STATS>(bm, bn, p, grid, R.st); break;
-        default: throw Error(DMX_E_INTERNAL, "bad src mode");
-      }
+      if (src_mode == SRC_NCHW) launch_ig_tiles<SRC_NCHW, EPI_STATS>(bm, bn, p, grid, R.st);
+      else launch_ig_tiles<SRC_PLAIN, EPI_STATS>(bm, bn, p, grid, R.st);
       break;
     case EPI_BIAS: launch_ig_tiles<SRC_PLAIN, EPI_BIAS>(bm, bn, p, grid, R.st); break;
     case EPI_BIAS_GELU: launch_ig_tiles<SRC_PLAIN, EPI_BIAS_GELU>(bm, bn, p, grid, R.st); break;
@@ -582,32 +610,37 @@ static void gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, co
   }
   R.end();
   HIPCHK(hipGetLastError());
+  return rrows;
 }
 
-static void gn_finalize(Run& R, const float2* rowpart, float2* stats, int N, int HW, int nseg, int G, int C) {
+static void gn_finalize(Run& R, const float2* rowpart, float2* stats, int N, int rrows, int nseg, int G, int C,
+                        int HWo) {
   if (R.plan) return;
-  R.begin("gn_finalize_kernel", 0.0, 8.0 * (double)N * HW * nseg);
-  gn_finalize_kernel<<<N * G, 256, 0, R.st>>>(rowpart, stats, HW, nseg, G, C, 1e-5f);
+  R.begin("gn_finalize_kernel", 0.0, 8.0 * (double)N * rrows * nseg);
+  gn_finalize_kernel<<<N * G, 256, 0, R.st>>>(rowpart, stats, rrows, nseg, G, C, HWo, 1e-5f);
   R.end();
   HIPCHK(hipGetLastError());
 }
 
-static void finish(Run& R, const FinishParams& fp, int rmode) {
+// GroupNorm (+GELU | +residual GELU) (+emb) materialisation; stats inline (rowpart, G=1)
+// or precomputed (stats).
+static void norm(Run& R, NormParams np, int N) {
   if (R.plan) return;
-  const size_t total = (size_t)fp.N * fp.H * fp.W * (fp.C / 4);
+  const size_t per = (size_t)np.HW * (np.C / 4);
+  const int chunks = (int)std::max<size_t>(1, std::min<size_t>(cdiv((int)per, 1024), cdiv(2048, N)));
+  R.begin("norm_kernel", 0.0, 4.0 * (double)N * np.HW * np.C * (np.res ? 3 : 2));
+  norm_kernel<<<dim3(chunks, N), 256, 0, R.st>>>(np);
+  R.end();
+  HIPCHK(hipGetLastError());
+}
+
+template <int SRC>
+static void prep(Run& R, const SrcDesc& s, float* out, int N, int H, int W, const char* name) {
+  if (R.plan) return;
+  const size_t total = (size_t)N * H * W * (s.C / 4);
   const int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
-  {
-    char nm[64];
-    std::snprintf(nm, sizeof nm, "finish_kernel<%d>", fp.has_res ? rmode : SRC_PLAIN);
-    R.begin(nm, 0.0, 4.0 * (double)total * 4 * (fp.has_res ? 3 : 2));
-  }
-  switch (rmode) {
-    case SRC_MAXPOOL: finish_kernel<SRC_MAXPOOL><<<blocks, 256, 0, R.st>>>(fp); break;
-    case SRC_UPCAT: finish_kernel<SRC_UPCAT><<<blocks, 256, 0, R.st>>>(fp); break;
-    case SRC_GNACT: finish_kernel<SRC_GNACT><<<blocks, 256, 0, R.st>>>(fp); break;
-    case SRC_NCHW: finish_kernel<SRC_NCHW><<<blocks, 256, 0, R.st>>>(fp); break;
-    default: finish_kernel<SRC_PLAIN><<<blocks, 256, 0, R.st>>>(fp); break;
-  }
+  R.begin(name, 0.0, 4.0 * (double)N * H * W * s.C * (SRC == SRC_MAXPOOL ? 5 : 2));
+  prep_kernel<SRC><<<blocks, 256, 0, R.st>>>(s, out, N, H, W);
   R.end();
   HIPCHK(hipGetLastError());
 }
@@ -622,45 +655,50 @@ static SrcDesc plain_src(const float* p, int C) {
   return s;
 }
 
-// ResBlock (models/unet_cond.py:10-30): conv -> GN -> GELU -> conv -> GN [-> GELU(x + .)] [+ emb]
+static NormParams norm_params(const float* raw, const float2* rowpart, int nseg, int rrows, const float* g,
+                              const float* b, int C, int HW, float* out) {
+  NormParams np;
+  std::memset(&np, 0, sizeof(np));
+  np.raw = raw;
+  np.rowpart = rowpart;
+  np.nseg = nseg;
+  np.rrows = rrows;
+  np.gamma = g;
+  np.beta = b;
+  np.C = C;
+  np.G = 1;
+  np.HW = HW;
+  np.out = out;
+  return np;
+}
+
+// ResBlock (models/unet_cond.py:10-30):
+//   conv1 (+row stats) -> GN+GELU (materialised) -> conv2 (+row stats) -> GN [-> GELU(x + .)] [+ emb]
+// `in` is a plain NHWC tensor (or the NCHW network input for `inc`); it doubles as the residual.
 static float* resblock(Run& R, const ResW& w, const SrcDesc& in, int mode, int N, int H, int W, bool residual,
                        const float* emb, int emb_stride, int emb_off) {
-  const int M = N * H * W;
+  const int M = N * H * W, HW = H * W;
   const int seg = 32;
   float* r1 = R.ws.get<float>((size_t)M * w.mid);
   float2* rp1 = R.ws.get<float2>((size_t)M * (w.mid / seg));
-  float2* st1 = R.ws.get<float2>(N);
-  gemm(R, in, mode, N, H, W, w.c1, EPI_STATS, r1, nullptr, rp1, seg);
-  gn_finalize(R, rp1, st1, N, H * W, w.mid / seg, 1, w.mid);
-  SrcDesc s2 = plain_src(r1, w.mid);
-  s2.stats = st1;
-  s2.gamma = w.g1.p;
-  s2.beta = w.b1.p;
-  s2.act = 1;
+  float* a1 = R.ws.get<float>((size_t)M * w.mid);
   float* r2 = R.ws.get<float>((size_t)M * w.cout);
   float2* rp2 = R.ws.get<float2>((size_t)M * (w.cout / seg));
-  float2* st2 = R.ws.get<float2>(N);
-  gemm(R, s2, SRC_GNACT, N, H, W, w.c2, EPI_STATS, r2, nullptr, rp2, seg);
-  gn_finalize(R, rp2, st2, N, H * W, w.cout / seg, 1, w.cout);
   float* out = R.ws.get<float>((size_t)M * w.cout);
-  FinishParams fp;
-  std::memset(&fp, 0, sizeof(fp));
-  fp.raw = r2;
-  fp.stats = st2;
-  fp.gamma = w.g2.p;
-  fp.beta = w.b2.p;
-  fp.G = 1;
-  fp.C = w.cout;
-  fp.H = H;
-  fp.W = W;
-  fp.N = N;
-  fp.res = in;
-  fp.has_res = residual ? 1 : 0;
-  fp.emb = emb;
-  fp.emb_stride = emb_stride;
-  fp.emb_off = emb_off;
-  fp.out = out;
-  finish(R, fp, residual ? mode : SRC_PLAIN);
+  const int rr1 = gemm(R, in, mode, N, H, W, w.c1, EPI_STATS, r1, nullptr, rp1, seg);
+  NormParams n1 = norm_params(r1, rp1, w.mid / seg, rr1, w.g1.p, w.b1.p, w.mid, HW, a1);
+  n1.act = 1;
+  norm(R, n1, N);
+  const int rr2 = gemm(R, plain_src(a1, w.mid), SRC_PLAIN, N, H, W, w.c2, EPI_STATS, r2, nullptr, rp2, seg);
+  NormParams n2 = norm_params(r2, rp2, w.cout / seg, rr2, w.g2.p, w.b2.p, w.cout, HW, out);
+  if (residual) {
+    if (mode != SRC_PLAIN) throw Error(DMX_E_INTERNAL, "residual ResBlock needs a plain input");
+    n2.res = in.src0;
+  }
+  n2.emb = emb;
+  n2.emb_stride = emb_stride;
+  n2.emb_off = emb_off;
+  norm(R, n2, N);
   R.tap(R.layer + ".r1", r1, (size_t)M * w.mid);
   R.tap(R.layer, out, (size_t)M * w.cout);
   return out;
@@ -788,7 +826,9 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
     mp.Ws = cw;
     const int nh = ch / 2, nw = cw / 2;
     R.layer = "down" + std::to_string(i + 1) + ".0";
-    float* h0 = resblock(R, m->down[i].r0, mp, SRC_MAXPOOL, N, nh, nw, true, nullptr, 0, 0);
+    float* pooled = R.ws.get<float>((size_t)N * nh * nw * cc);
+    prep<SRC_MAXPOOL>(R, mp, pooled, N, nh, nw, "prep_kernel<2>");
+    float* h0 = resblock(R, m->down[i].r0, plain_src(pooled, cc), SRC_PLAIN, N, nh, nw, true, nullptr, 0, 0);
     R.layer = "down" + std::to_string(i + 1) + ".1";
     float* h1 = resblock(R, m->down[i].r1, plain_src(h0, cc), SRC_PLAIN, N, nh, nw, false, emb, m->hsum,
                          m->down[i].emb_off);
@@ -817,7 +857,9 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
     u.padL = dx > 0 ? dx / 2 : 0;
     REQUIRE(u.C == m->up[i].r0.cin, "up: channel mismatch");
     R.layer = "up" + std::to_string(i + 1) + ".0";
-    float* h0 = resblock(R, m->up[i].r0, u, SRC_UPCAT, N, sh[si], sw[si], true, nullptr, 0, 0);
+    float* cat = R.ws.get<float>((size_t)N * sh[si] * sw[si] * u.C);
+    prep<SRC_UPCAT>(R, u, cat, N, sh[si], sw[si], "prep_kernel<3>");
+    float* h0 = resblock(R, m->up[i].r0, plain_src(cat, u.C), SRC_PLAIN, N, sh[si], sw[si], true, nullptr, 0, 0);
     R.layer = "up" + std::to_string(i + 1) + ".1";
     float* h1 = resblock(R, m->up[i].r1, plain_src(h0, u.C), SRC_PLAIN, N, sh[si], sw[si], false, emb, m->hsum,
                          m->up[i].emb_off);
@@ -918,7 +960,9 @@ static void validate_step(dmx_model* m, const dmx_step_args* a) {
     REQUIRE((a->vals == nullptr) == (a->mask == nullptr), "vals and mask must be given together");
 }
 
-// VAE decoder (models/vae.py:35-49,64-69) on one chunk of n latents.
+// VAE decoder (models/vae.py:35-49,64-69) on one chunk of n latents:
+// [conv3x3 | ConvT-phase GEMM] (+row stats) -> GN(8) finalize -> GN+GELU materialised, x6, then
+// conv3x3 64->3 + sigmoid + uint8 in vae_tail_kernel.
 static void vae_body(Run& R, const float* z, float* img, uint8_t* u8, int n, int h, int w) {
   dmx_model* m = R.m;
   const int G = 8;
@@ -927,53 +971,36 @@ static void vae_body(Run& R, const float* z, float* img, uint8_t* u8, int n, int
   s.scale = 0.18215f;
   int mode = SRC_NCHW;
   int H = h, W = w;
-  const float* raw = nullptr;
-  const float2* stats = nullptr;
-  int C = 4;
+  const float* act = nullptr;
   for (int stage = 0; stage < 6; ++stage) {
     const bool convt = stage & 1;
     const ConvW& cw = convt ? m->vconvt[stage / 2] : m->vconv[stage / 2];
     const int Ho = convt ? 2 * H : H, Wo = convt ? 2 * W : W;
     const int Mo = n * Ho * Wo;
     const int seg = std::min(32, cw.cout / G);
+    R.layer = "dec" + std::to_string(stage);
     float* r = R.ws.get<float>((size_t)Mo * cw.cout);
     float2* rp = R.ws.get<float2>((size_t)Mo * (cw.cout / seg));
     float2* st = R.ws.get<float2>((size_t)n * G);
-    if (stage > 0) {
-      s = plain_src(raw, C);
-      s.stats = stats;
-      s.gamma = m->vg[stage - 1].p;
-      s.beta = m->vb[stage - 1].p;
-      s.G = G;
-      s.act = 1;
-      mode = SRC_GNACT;
-    }
-    gemm(R, s, mode, n, H, W, cw, EPI_STATS, r, nullptr, rp, seg);
-    gn_finalize(R, rp, st, n, Ho * Wo, cw.cout / seg, G, cw.cout);
-    raw = r;
-    stats = st;
-    C = cw.cout;
+    float* a = R.ws.get<float>((size_t)Mo * cw.cout);
+    const int rr = gemm(R, s, mode, n, H, W, cw, EPI_STATS, r, nullptr, rp, seg);
+    gn_finalize(R, rp, st, n, rr, cw.cout / seg, G, cw.cout, Ho * Wo);
+    NormParams np = norm_params(r, nullptr, 0, 0, m->vg[stage].p, m->vb[stage].p, cw.cout, Ho * Wo, a);
+    np.stats = st;
+    np.G = G;
+    np.act = 1;
+    norm(R, np, n);
+    act = a;
+    s = plain_src(a, cw.cout);
+    mode = SRC_PLAIN;
     H = Ho;
     W = Wo;
   }
-  float* act = R.ws.get<float>((size_t)n * H * W * C);
-  FinishParams fp;
-  std::memset(&fp, 0, sizeof(fp));
-  fp.raw = raw;
-  fp.stats = stats;
-  fp.gamma = m->vg[5].p;
-  fp.beta = m->vb[5].p;
-  fp.G = G;
-  fp.C = C;
-  fp.H = H;
-  fp.W = W;
-  fp.N = n;
-  fp.act = 1;
-  fp.out = act;
-  finish(R, fp, SRC_PLAIN);
   if (R.plan) return;
   dim3 grid(cdiv(H * W, 256), n);
+  R.begin("vae_tail_kernel", 2.0 * n * H * W * 3 * 576, 4.0 * (double)n * H * W * (64 + 3) + (double)n * H * W * 3);
   vae_tail_kernel<<<grid, 256, 0, R.st>>>(act, m->vconv[3].B, m->vconv[3].bias, n, H, W, img, u8);
+  R.end();
   HIPCHK(hipGetLastError());
 }
 

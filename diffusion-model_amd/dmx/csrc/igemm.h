@@ -37,8 +37,12 @@ struct IgemmParams {
   const float* bias;  // [Cout] or null
   float* out;         // NHWC [N][Hout][Wout][Cout]
   const float* res;   // EPI_BIAS_RES residual, same layout as out
-  float2* rowpart;    // EPI_STATS: [N*Hout*Wout][Cout/seg]
+  float2* rowpart;    // EPI_STATS: GroupNorm partials, see stats_row()
   int seg;            // columns per GroupNorm partial (power of two, <= 32)
+  int rgrp;           // rows per partial: 32 (needs H*W % 32 == 0) or 1
+  int nphase;         // phases of this GEMM (1, or 4 for ConvT)
+  int ksplit;         // EPI_PARTIAL: K-tiles per split (blockIdx.z = split; phases must be 1)
+  float* partial;     // EPI_PARTIAL: [splits][M][Cout]
 };
 
 constexpr int IG_BK = 16;
@@ -55,7 +59,7 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(const IgemmParams p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int phase = blockIdx.z;
+  const int phase = EPI == EPI_PARTIAL ? 0 : blockIdx.z;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const int q = tid & 3;          // float4 piece within a 16-wide K slice
   const int rbase = tid >> 2;     // staging row (+ i * 64)
@@ -109,15 +113,19 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(const IgemmParams p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int nK = p.Kpad / IG_BK;
-  load_tile(0);
+  int kbeg = 0, nK = p.Kpad / IG_BK;
+  if constexpr (EPI == EPI_PARTIAL) {
+    kbeg = blockIdx.z * p.ksplit;
+    nK = min(nK - kbeg, p.ksplit);
+  }
+  load_tile(kbeg);
   store_tile(0);
   __syncthreads();
 
   const int fr = lane & 31, fh = lane >> 5;
   for (int kt = 0; kt < nK; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < nK) load_tile(kt + 1);
+    if (kt + 1 < nK) load_tile(kbeg + kt + 1);
     floatx4 a[TM][2], b[TN][2];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -143,18 +151,38 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(const IgemmParams p) {
   }
 
   // ---- epilogue -------------------------------------------------------------
-  const int HWo = p.Hout * p.Wout;
-  const int nseg = p.Cout / (EPI == EPI_STATS ? p.seg : 1);
+  if constexpr (EPI == EPI_PARTIAL) {
+    float* dst = p.partial + (size_t)blockIdx.z * p.M * p.Cout;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = n0 + wn * WN + j * 32 + fr;
+          if (m < p.M && col < p.Cout) dst[(size_t)m * p.Cout + col] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+  const int nseg = EPI == EPI_STATS ? p.Cout / p.seg : 1;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
+    float s1[TN], s2[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) s1[j] = s2[j] = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = (r & 3) + 8 * (r >> 2) + 4 * fh;
       const int m = m0 + wm * WM + i * 32 + row;
       const bool mv = m < p.M;
       size_t oidx = 0;
+      int nn = 0, rr = 0;
       if (mv) {
-        const int nn = m / HW, rr = m - nn * HW, y = rr / p.W, x = rr - y * p.W;
+        nn = m / HW;
+        rr = m - nn * HW;
+        const int y = rr / p.W, x = rr - y * p.W;
         oidx = ((size_t)nn * p.Hout + (y * p.osy + p.py[phase])) * p.Wout + (x * p.osx + p.px[phase]);
       }
 #pragma unroll
@@ -169,15 +197,92 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(const IgemmParams p) {
         }
         if (v) p.out[oidx * p.Cout + col] = val;
         if constexpr (EPI == EPI_STATS) {
-          float s1 = v ? val : 0.f, s2 = v ? val * val : 0.f;
-          for (int o = 1; o < p.seg; o <<= 1) {
-            s1 += __shfl_xor(s1, o, 64);
-            s2 += __shfl_xor(s2, o, 64);
+          const float a1 = v ? val : 0.f;
+          if (p.rgrp == 32) {  // accumulate the lane's 16 rows, reduce across lanes below
+            s1[j] += a1;
+            s2[j] += a1 * a1;
+          } else {
+            float t1 = a1, t2 = a1 * a1;
+            for (int o = 1; o < p.seg; o <<= 1) {
+              t1 += __shfl_xor(t1, o, 64);
+              t2 += __shfl_xor(t2, o, 64);
+            }
+            const size_t er = ((size_t)nn * p.nphase + phase) * HW + rr;
+            if (v && (fr & (p.seg - 1)) == 0) p.rowpart[er * nseg + col / p.seg] = make_float2(t1, t2);
           }
-          if (v && (fr & (p.seg - 1)) == 0) p.rowpart[oidx * nseg + col / p.seg] = make_float2(s1, s2);
         }
       }
     }
+    if constexpr (EPI == EPI_STATS) {
+      if (p.rgrp == 32) {
+        const int mb = m0 + wm * WM + i * 32;  // 32-row group, within one sample (HW % 32 == 0)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          float t1 = s1[j], t2 = s2[j];
+          for (int o = 1; o < p.seg; o <<= 1) {
+            t1 += __shfl_xor(t1, o, 64);
+            t2 += __shfl_xor(t2, o, 64);
+          }
+          t1 += __shfl_xor(t1, 32, 64);
+          t2 += __shfl_xor(t2, 32, 64);
+          const int col = n0 + wn * WN + j * 32 + fr;
+          if (mb < p.M && col < p.Cout && fh == 0 && (fr & (p.seg - 1)) == 0) {
+            const int nn = mb / HW, lg = (mb - nn * HW) / 32;
+            const size_t er = ((size_t)nn * p.nphase + phase) * (HW / 32) + lg;
+            p.rowpart[er * nseg + col / p.seg] = make_float2(t1, t2);
+          }
+        }
+      }
+    }
+  }
+}
+
+// Split-K reduction + the epilogue the GEMM would have applied (deterministic:
+// slabs summed in split order).  One thread per 4 columns of a row; a 32-column
+// GroupNorm segment is 8 consecutive threads.
+struct SplitkParams {
+  const float* partial; int splits; int M, Cout;
+  const float* bias; const float* res; float* out; float2* rowpart; int seg; int epi;
+};
+
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const SplitkParams p) {
+  const int C4 = p.Cout / 4;
+  const size_t total = (size_t)p.M * C4;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const bool valid = i < total;
+  const size_t m = valid ? i / C4 : 0;
+  const int c = valid ? (int)(i % C4) * 4 : 0;
+  floatx4 v = {0.f, 0.f, 0.f, 0.f};
+  if (valid) {
+    for (int s = 0; s < p.splits; ++s) {
+      const floatx4 a = ld4(p.partial + ((size_t)s * p.M + m) * p.Cout + c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] += a[j];
+    }
+    if (p.bias != nullptr) {
+      const floatx4 b = ld4(p.bias + c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] += b[j];
+    }
+    if (p.epi == EPI_BIAS_GELU) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = gelu(v[j]);
+    } else if (p.epi == EPI_BIAS_RES) {
+      const floatx4 r = ld4(p.res + m * p.Cout + c);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] += r[j];
+    }
+    *reinterpret_cast<floatx4*>(p.out + m * p.Cout + c) = v;
+  }
+  if (p.epi == EPI_STATS) {
+    // lanes of one segment are consecutive (seg/4 threads; Cout % seg == 0)
+    float s1 = valid ? v[0] + v[1] + v[2] + v[3] : 0.f;
+    float s2 = valid ? v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3] : 0.f;
+    for (int o = 1; o < p.seg / 4; o <<= 1) {
+      s1 += __shfl_xor(s1, o, 64);
+      s2 += __shfl_xor(s2, o, 64);
+    }
+    if (valid && (c % p.seg) == 0) p.rowpart[m * (p.Cout / p.seg) + c / p.seg] = make_float2(s1, s2);
   }
 }
 

@@ -82,16 +82,17 @@ __global__ __launch_bounds__(256) void embed_kernel(const EmbedParams p) {
 // the conv epilogue.  Sums are combined in double (deterministic order).
 // nn.GroupNorm eps = 1e-5 (models/unet_cond.py:20, models/vae.py:36).
 // ---------------------------------------------------------------------------
-// Finalize with the channel count known (element count = HW * C / G).
-__global__ __launch_bounds__(256) void gn_finalize_kernel(const float2* rowpart, float2* stats, int HW, int nseg,
-                                                            int G, int C, float eps) {
+// rowpart layout: [n][R rows][nseg] (R = partial rows per sample); elements per
+// group = HWo * C / G.
+__global__ __launch_bounds__(256) void gn_finalize_kernel(const float2* rowpart, float2* stats, int R, int nseg,
+                                                           int G, int C, int HWo, float eps) {
   const int ng = blockIdx.x, n = ng / G, g = ng % G;
   const int spg = nseg / G;
-  const int cnt_rows = HW * spg;
+  const int cnt = R * spg;
   double s1 = 0.0, s2 = 0.0;
-  for (int i = threadIdx.x; i < cnt_rows; i += 256) {
+  for (int i = threadIdx.x; i < cnt; i += 256) {
     const int r = i / spg, sg = g * spg + (i - r * spg);
-    const float2 v = rowpart[((size_t)n * HW + r) * nseg + sg];
+    const float2 v = rowpart[((size_t)n * R + r) * nseg + sg];
     s1 += (double)v.x;
     s2 += (double)v.y;
   }
@@ -107,47 +108,80 @@ __global__ __launch_bounds__(256) void gn_finalize_kernel(const float2* rowpart,
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    const double cnt = (double)HW * (double)(C / G);
-    const double mean = r1[0] / cnt;
-    double var = r2[0] / cnt - mean * mean;
+    const double cntd = (double)HWo * (double)(C / G);
+    const double mean = r1[0] / cntd;
+    double var = r2[0] / cntd - mean * mean;
     var = var < 0.0 ? 0.0 : var;
     stats[ng] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)eps)));
   }
 }
 
 // ---------------------------------------------------------------------------
-// ResBlock / decoder-stage finish (materialises the block output, NHWC):
-//   y = GN(raw)                     (non-residual ResBlock, models/unet_cond.py:30)
-//   y = GELU(x + GN(raw))           (residual ResBlock, models/unet_cond.py:28)
-//   y = GELU(GN(raw))               (VAE GN+GELU, models/vae.py:36-48)
-//   y += emb[n][c]                  (Down/Up "+ emb", models/unet_cond.py:69-70,99-100)
-// The residual input x is re-derived from its fused source (max-pool, up+cat).
+// GroupNorm application, fused with the statistics reduction for G == 1
+// (models/unet_cond.py:20-28):
+//   out = GN(raw)                    (act=0, no res)     non-residual ResBlock output
+//   out = GELU(GN(raw))              (act=1, no res)     mid-block activation / VAE stage
+//   out = GELU(res + GN(raw))        (res != null)       residual ResBlock output
+//   out += emb[n][emb_off + c]       (emb != null)       Down/Up "+ emb" (unet_cond.py:69,99)
+// Stats: either precomputed (stats != null, any G) or reduced here from the conv
+// epilogue's per-row partials (rowpart, G == 1): every block re-reduces its sample's
+// partials (<= 32 KB, L2-resident) in double, in a fixed order, then normalises its
+// chunk of the sample.  grid = (chunks, N).
 // ---------------------------------------------------------------------------
-struct FinishParams {
-  const float* raw; const float2* stats; const float* gamma; const float* beta; int G;
-  int C, H, W, N;
-  SrcDesc res;       // residual source (valid if has_res)
-  int has_res;
-  int act;           // GELU after GN (no residual)
+struct NormParams {
+  const float* raw; const float2* rowpart; int nseg; int rrows; const float2* stats;
+  const float* gamma; const float* beta;
+  int C, G, HW;
+  const float* res; int act;
   const float* emb; int emb_stride; int emb_off;
   float* out;
 };
 
-template <int RSRC>
-__global__ __launch_bounds__(256) void finish_kernel(const FinishParams p) {
+__global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
+  const int n = blockIdx.y;
+  __shared__ double r1[256], r2[256];
+  __shared__ float2 st_s;
+  if (p.rowpart != nullptr) {
+    const int cnt = p.rrows * p.nseg;
+    const float2* rp = p.rowpart + (size_t)n * cnt;
+    double s1 = 0.0, s2 = 0.0;
+    for (int i = threadIdx.x; i < cnt; i += 256) {
+      const float2 v = rp[i];
+      s1 += (double)v.x;
+      s2 += (double)v.y;
+    }
+    r1[threadIdx.x] = s1;
+    r2[threadIdx.x] = s2;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (threadIdx.x < o) {
+        r1[threadIdx.x] += r1[threadIdx.x + o];
+        r2[threadIdx.x] += r2[threadIdx.x + o];
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      const double cntd = (double)p.HW * (double)p.C;
+      const double mean = r1[0] / cntd;
+      double var = r2[0] / cntd - mean * mean;
+      var = var < 0.0 ? 0.0 : var;
+      st_s = make_float2((float)mean, (float)(1.0 / sqrt(var + 1e-5)));
+    }
+    __syncthreads();
+  }
   const int C4 = p.C / 4;
-  const size_t total = (size_t)p.N * p.H * p.W * C4;
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+  const size_t per = (size_t)p.HW * C4;
+  const size_t chunk = (per + gridDim.x - 1) / gridDim.x;
+  const size_t beg = blockIdx.x * chunk, end = min(per, beg + chunk);
+  const size_t base = (size_t)n * p.HW * p.C;
+  const int cpg = p.C / p.G;
+  for (size_t i = beg + threadIdx.x; i < end; i += 256) {
     const int c = (int)(i % C4) * 4;
-    const size_t pix = i / C4;
-    const int n = (int)(pix / ((size_t)p.H * p.W));
-    const int rr = (int)(pix - (size_t)n * p.H * p.W);
-    const int y = rr / p.W, x = rr - y * p.W;
-    floatx4 v = ld4(p.raw + pix * p.C + c);
-    const int g = c / (p.C / p.G);
-    floatx4 o = gn_apply4(v, p.stats[n * p.G + g], p.gamma, p.beta, c, 0);
-    if (p.has_res) {
-      floatx4 r = load_src4<RSRC>(p.res, n, y, x, c, p.H, p.W);
+    const size_t off = base + i * 4;
+    const float2 st = p.rowpart != nullptr ? st_s : p.stats[n * p.G + c / cpg];
+    floatx4 o = gn_apply4(ld4(p.raw + off), st, p.gamma, p.beta, c, 0);
+    if (p.res != nullptr) {
+      const floatx4 r = ld4(p.res + off);
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = gelu(r[j] + o[j]);
     } else if (p.act) {
@@ -155,11 +189,27 @@ __global__ __launch_bounds__(256) void finish_kernel(const FinishParams p) {
       for (int j = 0; j < 4; ++j) o[j] = gelu(o[j]);
     }
     if (p.emb != nullptr) {
-      floatx4 e = ld4(p.emb + (size_t)n * p.emb_stride + p.emb_off + c);
+      const floatx4 e = ld4(p.emb + (size_t)n * p.emb_stride + p.emb_off + c);
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] += e[j];
     }
-    *reinterpret_cast<floatx4*>(p.out + pix * p.C + c) = o;
+    *reinterpret_cast<floatx4*>(p.out + off) = o;
+  }
+}
+
+// Materialise a fused source (2x2 max-pool, bilinear-x2 + pad + concat) as a plain
+// NHWC tensor [N][H][W][C] (models/unet_cond.py:58, 88-97).
+template <int SRC>
+__global__ __launch_bounds__(256) void prep_kernel(const SrcDesc s, float* out, int N, int H, int W) {
+  const int C4 = s.C / 4;
+  const size_t total = (size_t)N * H * W * C4;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const int c = (int)(i % C4) * 4;
+    const size_t pix = i / C4;
+    const int n = (int)(pix / ((size_t)H * W));
+    const int rr = (int)(pix - (size_t)n * H * W);
+    const int y = rr / W, x = rr - y * W;
+    *reinterpret_cast<floatx4*>(out + pix * s.C + c) = load_src4<SRC>(s, n, y, x, c, H, W);
   }
 }
 
@@ -380,10 +430,16 @@ struct StepTailParams {
   uint64_t seed; int64_t sample_offset;
 };
 
-#pragma clang fp contract(off)
+// One IEEE rounding per reference op: the product is forced through a register
+// (opaque asm barrier) so no multiply-add pair can be contracted into an FMA,
+// whatever the -ffp-contract mode of the including code.
+DMX_DEV float rnd(float v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
 DMX_DEV float ddpm_elem(float x, float eps, float c1, float c2, float sd, float nz) {
-  const float mu = __fdiv_rn(__fsub_rn(x, __fmul_rn(c1, eps)), c2);
-  return __fadd_rn(mu, __fmul_rn(nz, sd));
+  const float mu = rnd(x - rnd(c1 * eps)) / c2;
+  return mu + rnd(nz * sd);
 }
 
 __global__ __launch_bounds__(256) void step_tail_kernel(const StepTailParams p) {
@@ -409,8 +465,8 @@ __global__ __launch_bounds__(256) void step_tail_kernel(const StepTailParams p) 
         const floatx4 w = ld4(p.w + c * 64 + k);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          eu[c] = __fadd_rn(eu[c], __fmul_rn(w[j], a[j]));
-          ec[c] = __fadd_rn(ec[c], __fmul_rn(w[j], bb[j]));
+          eu[c] += w[j] * a[j];
+          ec[c] += w[j] * bb[j];
         }
       }
     }
@@ -431,7 +487,7 @@ __global__ __launch_bounds__(256) void step_tail_kernel(const StepTailParams p) 
   }
   const float c1 = p.c1[t - 1], c2 = p.c2[t - 1], sd = p.sd[t - 1];
   for (int c = 0; c < Co; ++c) {
-    const float eps = p.cfg ? __fadd_rn(eu[c], __fmul_rn(p.guidance, __fsub_rn(ec[c], eu[c]))) : eu[c];
+    const float eps = p.cfg ? eu[c] + rnd(p.guidance * rnd(ec[c] - eu[c])) : eu[c];
     const size_t idx = ((size_t)n * Co + c) * p.HW + pix;
     p.x_out[idx] = ddpm_elem(p.x[idx], eps, c1, c2, sd, nz[c]);
   }
@@ -450,7 +506,7 @@ __global__ __launch_bounds__(256) void out_head_kernel(const float* feat, const 
     for (int c = 0; c < Co; ++c) {
       const floatx4 ww = ld4(w + c * 64 + k);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[c] = __fadd_rn(acc[c], __fmul_rn(ww[j], a[j]));
+      for (int j = 0; j < 4; ++j) acc[c] += ww[j] * a[j];
     }
   }
   for (int c = 0; c < Co; ++c) eps[((size_t)n * Co + c) * HW + pix] = acc[c];
@@ -513,7 +569,7 @@ __global__ __launch_bounds__(256) void vae_tail_kernel(const float* in, const fl
   for (int co = 0; co < 3; ++co) {
     if (img != nullptr) img[((size_t)n * 3 + co) * H * W + pix] = o[co];
     if (u8 != nullptr) {
-      float q = __fmul_rn(o[co], 255.f);
+      float q = rnd(o[co] * 255.f);
       q = fminf(fmaxf(q, 0.f), 255.f);
       u8[((size_t)n * H * W + pix) * 3 + co] = (uint8_t)q;
     }
