@@ -1,0 +1,126 @@
+"""Sample-sharded multi-GPU sampling (one process per GPU, torch.distributed / RCCL).
+
+The CFG loop has no cross-sample coupling (GroupNorm/LayerNorm are per sample), so a
+job of B samples is split into contiguous shards [start, end) per rank:
+
+  * C1 — frozen weights are broadcast once from rank 0 (``broadcast_module``);
+  * no per-step collective;
+  * C2 — decoded images / latents are gathered once at the end (``gather_rows``).
+
+Noise stays shard-invariant in both modes:
+  * ``"device"``: Philox keyed by the *global* sample index (``sample_offset = start``);
+  * ``"host"``: every rank draws the full global (B, C, H, W) tensor from the CPU
+    generator each step and keeps its slice — torch.randn is prefix-stable, so every
+    sample sees exactly the draw the single-process reference would give it.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def world() -> Tuple[int, int]:
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+def shard_range(total: int, world_size: int, rank: int) -> Tuple[int, int]:
+    """Contiguous, balanced [start, end) of `total` samples for `rank` (first ranks get the extra)."""
+    base, extra = divmod(total, world_size)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def broadcast_module(module: torch.nn.Module, src: int = 0) -> None:
+    """C1: broadcast every parameter/buffer of `module` from `src` (once per job)."""
+    ws, _ = world()
+    if ws == 1:
+        return
+    with torch.no_grad():
+        for t in list(module.parameters()) + list(module.buffers()):
+            dist.broadcast(t.data, src=src)
+
+
+def gather_rows(local: torch.Tensor, total: int, dst: int = 0) -> Optional[torch.Tensor]:
+    """C2: concatenate every rank's shard (dim 0) on `dst` in global order; None elsewhere.
+    Shards may differ by one row; they are padded to a common size for the collective."""
+    ws, rank = world()
+    if ws == 1:
+        return local
+    sizes = [shard_range(total, ws, r)[1] - shard_range(total, ws, r)[0] for r in range(ws)]
+    mx = max(sizes)
+    pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    pad[: local.shape[0]] = local
+    bufs = [torch.empty_like(pad) for _ in range(ws)]
+    dist.all_gather(bufs, pad)
+    if rank != dst:
+        return None
+    return torch.cat([b[:s] for b, s in zip(bufs, sizes)], dim=0)
+
+
+def host_noise_slice(shape_global, start: int, end: int, device) -> torch.Tensor:
+    """One global CPU-generator draw, sliced to this shard (reference draw order)."""
+    return torch.randn(tuple(shape_global))[start:end].to(device)
+
+
+def sharded_loop(step: Callable[[torch.Tensor, int, Optional[torch.Tensor]], torch.Tensor], x_global_shape,
+                 T: int, device, noise_source: str = "host") -> torch.Tensor:
+    """Run the T loop on this rank's shard.
+
+    step(x_shard, t, noise_shard_or_None) -> x_shard'.  In host mode x_T and every
+    per-step noise are drawn globally and sliced; returns this rank's final shard."""
+    ws, rank = world()
+    s, e = shard_range(int(x_global_shape[0]), ws, rank)
+    x = host_noise_slice(x_global_shape, s, e, device)  # x_T (diff.py:327)
+    for i in range(T, 0, -1):
+        noise = host_noise_slice(x_global_shape, s, e, device) if noise_source == "host" else None
+        x = step(x, i, noise)
+    return x
+
+
+class ShardedCondSampler:
+    """Multi-GPU ``sample_latent_cond``: same arguments, this rank's shard runs on its GPU,
+    rank 0 receives all decoded uint8 images (HWC) or latents."""
+
+    def __init__(self, diffuser, model, vae=None):
+        self.d, self.model, self.vae = diffuser, model, vae
+
+    def sample(self, class_counts, z_shape, guidance_scale: float = 3.0, null_label: int = 0, cond=None,
+               cond_mask=None, decode: bool = True) -> Optional[torch.Tensor]:
+        ws, rank = world()
+        d = self.d
+        items = d._norm_counts(class_counts)
+        y_list: List[int] = []
+        for cls, num in items:
+            y_list += [cls] * num
+        B = len(y_list)
+        dev = torch.device(d.device)
+        vals, msk = d._build_cond(y_list, cond, cond_mask, None, None, dev)
+        s, e = shard_range(B, ws, rank)
+        y = torch.tensor(y_list[s:e], device=dev, dtype=torch.long)
+        v, m = vals[s:e].contiguous().float(), msk[s:e].contiguous().float()
+        C, H, W = z_shape
+        nm = self.model.native()
+        tables = d.coef_tables(dev, clamp_prev=True)
+        if d.noise_source == "device":
+            seed = torch.tensor([d._seed()], dtype=torch.long, device=dev)
+            if ws > 1:
+                dist.broadcast(seed, src=0)
+            x = torch.randn((B, C, H, W))[s:e].to(dev).contiguous()
+            t_dev = torch.full((1,), d.num_timesteps, dtype=torch.long, device=dev)
+            nm.sample_loop(x, t_dev, y, null_label, v, m, float(guidance_scale), tables, d.num_timesteps,
+                           seed=int(seed.item()), sample_offset=s, use_graph=d.use_graph)
+        else:
+            def step(xs, t, noise):
+                out = torch.empty_like(xs)
+                tt = torch.full((xs.shape[0],), t, dtype=torch.long, device=dev)
+                nm.step(xs, out, tt, y, null_label, v, m, float(guidance_scale), tables, noise)
+                return out
+            x = sharded_loop(step, (B, C, H, W), d.num_timesteps, dev, "host")
+        if decode and self.vae is not None:
+            _, u8 = self.vae.native().decode(x, want_img=False, want_u8=True)
+            return gather_rows(u8, B)
+        return gather_rows(x, B)
