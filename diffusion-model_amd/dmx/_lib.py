@@ -67,6 +67,8 @@ SIGNATURES = [
     ("dmx_model_destroy", _I, [_P]),
     ("dmx_model_set_tensor", _I, [_P, ctypes.c_char_p, _P, ctypes.POINTER(_I64), _I]),
     ("dmx_model_finalize", _I, [_P, _P]),
+    ("dmx_model_set_precision", _I, [_P, _I]),
+    ("dmx_model_get_precision", _I, [_P]),
     ("dmx_unet_forward", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
     ("dmx_step", _I, [_P, ctypes.POINTER(StepArgs), _P]),
     ("dmx_sample_loop", _I, [_P, ctypes.POINTER(StepArgs), _I, _I, _P]),

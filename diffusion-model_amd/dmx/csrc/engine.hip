@@ -2,6 +2,7 @@
 // step loop and the C ABI of include/dmx.h.
 #include "dmx.h"
 
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -12,6 +13,7 @@
 
 #include "common.h"
 #include "igemm.h"
+#include "igemm_x3.h"
 #include "kernels.h"
 
 namespace dmx {
@@ -156,7 +158,10 @@ static Keys model_keys(int kind, int in_ch, bool deep) {
 // Packed weights
 // ===========================================================================
 struct ConvW {
-  float* B = nullptr;
+  float* B = nullptr;           // fp32 [phases][npad][kpad]
+  _Float16* Bh = nullptr;       // split-precision planes (scaled by 1/inv_scale)
+  _Float16* Bl = nullptr;
+  float inv_scale = 1.f;
   float* bias = nullptr;
   int cin = 0, cout = 0, taps = 0, kpad = 0, npad = 0, phases = 1;
 };
@@ -236,6 +241,7 @@ struct dmx_model {
   bool has_graph = false;
   // debug taps: (name, device pointer into the workspace, element count, C)
   bool debug = false;
+  int prec = 1;  // 0: fp32 MFMA (exact fp32 products), 1: fp16 hi/lo x3 split MFMA
   std::vector<std::pair<std::string, std::pair<const float*, size_t>>> taps;
 };
 
@@ -267,6 +273,35 @@ struct Packer {
     return d;
   }
   Vec vec(const std::string& name) { return Vec{copy(name)}; }
+  // fp16 hi/lo planes of a packed fp32 B, scaled by 2^e so that max|w| * 2^e ~ 2^13
+  void split(ConvW& c) {
+    const size_t n = (size_t)c.phases * c.npad * c.kpad;
+    unsigned* d = nullptr;
+    HIPCHK(hipMalloc(&d, sizeof(unsigned)));
+    m->owned.push_back(d);
+    HIPCHK(hipMemsetAsync(d, 0, sizeof(unsigned), st));
+    absmax_kernel<<<256, 256, 0, st>>>(c.B, n, d);
+    HIPCHK(hipGetLastError());
+    unsigned bits = 0;
+    HIPCHK(hipMemcpyAsync(&bits, d, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    float mx;
+    std::memcpy(&mx, &bits, sizeof(float));
+    int e = 0;
+    if (mx > 0.f && std::isfinite(mx)) e = std::max(-8, std::min(24, (int)std::floor(std::log2(8192.0f / mx))));
+    const float scale = std::ldexp(1.0f, e);
+    c.inv_scale = std::ldexp(1.0f, -e);
+    void* h = nullptr;
+    void* l = nullptr;
+    HIPCHK(hipMalloc(&h, n * sizeof(_Float16)));
+    m->owned.push_back(h);
+    HIPCHK(hipMalloc(&l, n * sizeof(_Float16)));
+    m->owned.push_back(l);
+    c.Bh = static_cast<_Float16*>(h);
+    c.Bl = static_cast<_Float16*>(l);
+    split_weights_kernel<<<(int)std::min<size_t>((n + 255) / 256, 8192), 256, 0, st>>>(c.B, c.Bh, c.Bl, n, scale);
+    HIPCHK(hipGetLastError());
+  }
   void repack(float* dst, const float* src, int kind, int P, int npad, int kpad, int cout, int cin, int ks) {
     const size_t total = (size_t)P * npad * kpad;
     const int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
@@ -280,7 +315,7 @@ struct Packer {
     c.cin = cin_pad;
     c.cout = cout;
     c.taps = ks * ks;
-    c.kpad = rup(c.taps * cin_pad, IG_BK);
+    c.kpad = rup(c.taps * cin_pad, X3_BK);
     c.npad = rup(cout, 128);
     c.B = alloc((size_t)c.npad * c.kpad);
     if (cin_pad == cin) {
@@ -295,6 +330,7 @@ struct Packer {
       repack(c.B, tmp, 0, 1, c.npad, c.kpad, cout, cin_pad, ks);
     }
     if (!b.empty()) c.bias = copy(b);
+    split(c);
     return c;
   }
   ConvW linear(const std::string& w, const std::string& b, int fin, int fout) {
@@ -302,11 +338,12 @@ struct Packer {
     c.cin = fin;
     c.cout = fout;
     c.taps = 1;
-    c.kpad = rup(fin, IG_BK);
+    c.kpad = rup(fin, X3_BK);
     c.npad = rup(fout, 128);
     c.B = alloc((size_t)c.npad * c.kpad);
     repack(c.B, in(w).first, 1, 1, c.npad, c.kpad, fout, fin, 1);
     c.bias = copy(b);
+    split(c);
     return c;
   }
   ConvW convt(const std::string& w, const std::string& b, int cin, int cout) {
@@ -315,11 +352,12 @@ struct Packer {
     c.cout = cout;
     c.taps = 4;
     c.phases = 4;
-    c.kpad = rup(4 * cin, IG_BK);
+    c.kpad = rup(4 * cin, X3_BK);
     c.npad = rup(cout, 128);
     c.B = alloc((size_t)4 * c.npad * c.kpad);
     repack(c.B, in(w).first, 2, 4, c.npad, c.kpad, cout, cin, 4);
     c.bias = copy(b);
+    split(c);
     return c;
   }
   ResW res(const std::string& p, int cin, int cout, int mid = 0, int cin_pad = 0) {
@@ -510,6 +548,14 @@ static void launch_ig_tiles(int bm, int bn, const IgemmParams& p, dim3 grid, hip
   else launch_ig<64, 64, SRC, EPI>(p, grid, st);
 }
 
+template <int EPI>
+static void launch_x3_tiles(int bm, int bn, const X3Params& p, dim3 grid, hipStream_t st) {
+  if (bm == 128 && bn == 128) igemm_x3_kernel<128, 128, EPI><<<grid, 256, 0, st>>>(p);
+  else if (bm == 128) igemm_x3_kernel<128, 64, EPI><<<grid, 256, 0, st>>>(p);
+  else if (bn == 128) igemm_x3_kernel<64, 128, EPI><<<grid, 256, 0, st>>>(p);
+  else igemm_x3_kernel<64, 64, EPI><<<grid, 256, 0, st>>>(p);
+}
+
 // Implicit GEMM: conv3x3 (taps 9), ConvT phases (taps 4, phases 4), linear (taps 1).
 // Sources are plain NHWC (or the NCHW network input); grids too small to fill the
 // 256 CUs are split along K into deterministic slabs reduced by splitk_reduce_kernel.
@@ -522,10 +568,12 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   const int tiles128 = cdiv(M, 128) * cdiv(cw.cout, bn) * cw.phases;
   const int bm = tiles128 >= 512 ? 128 : 64;
   const int blocks = cdiv(M, bm) * cdiv(cw.cout, bn) * cw.phases;
-  const int nkt = cw.kpad / IG_BK;
+  const bool x3 = R.m->prec == 1 && src_mode == SRC_PLAIN && cw.Bh != nullptr;
+  const int bk = x3 ? X3_BK : IG_BK;
+  const int nkt = cw.kpad / bk;
   int splits = 1, ksplit = nkt;
-  if (cw.phases == 1 && blocks < 256 && nkt >= 32) {
-    splits = std::min(std::min(8, std::max(2, 512 / blocks)), nkt / 16);
+  if (cw.phases == 1 && blocks < 256 && nkt * bk >= 512) {
+    splits = std::min(std::min(8, std::max(2, 512 / blocks)), nkt * bk / 256);
     ksplit = cdiv(nkt, splits);
     splits = cdiv(nkt, ksplit);
   }
@@ -573,6 +621,12 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   p.nphase = cw.phases;
   if (s.C != cw.cin) throw Error(DMX_E_INTERNAL, "gemm: source channels != weight channels");
   if (src_mode != SRC_PLAIN && src_mode != SRC_NCHW) throw Error(DMX_E_INTERNAL, "gemm: unsupported source");
+  X3Params xp;
+  xp.g = p;
+  xp.Bh = cw.Bh;
+  xp.Bl = cw.Bl;
+  xp.inv_scale = cw.inv_scale;
+  const char* kname = x3 ? "igemm_x3_kernel" : "igemm_f32_kernel";
   const int creal = (src_mode == SRC_NCHW && s.C0) ? s.C0 : cw.cin;
   const double flops = 2.0 * (double)M * cw.phases * cw.cout * (double)cw.taps * creal;
   const double bytes = 4.0 * ((double)M * cw.phases * cw.cout + (double)M * s.C +
@@ -580,9 +634,11 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   char nm[96];
   if (splits > 1) {
     dim3 grid(cdiv(M, bm), cdiv(cw.cout, bn), splits);
-    std::snprintf(nm, sizeof nm, "igemm_f32_kernel<%d, %d, %d, %d>", bm, bn, src_mode, (int)EPI_PARTIAL);
+    if (x3) std::snprintf(nm, sizeof nm, "%s<%d, %d, %d>", kname, bm, bn, (int)EPI_PARTIAL);
+    else std::snprintf(nm, sizeof nm, "%s<%d, %d, %d, %d>", kname, bm, bn, src_mode, (int)EPI_PARTIAL);
     R.begin(nm, flops, bytes + 4.0 * splits * M * cw.cout);
-    if (src_mode == SRC_NCHW) launch_ig_tiles<SRC_NCHW, EPI_PARTIAL>(bm, bn, p, grid, R.st);
+    if (x3) launch_x3_tiles<EPI_PARTIAL>(bm, bn, xp, grid, R.st);
+    else if (src_mode == SRC_NCHW) launch_ig_tiles<SRC_NCHW, EPI_PARTIAL>(bm, bn, p, grid, R.st);
     else launch_ig_tiles<SRC_PLAIN, EPI_PARTIAL>(bm, bn, p, grid, R.st);
     R.end();
     HIPCHK(hipGetLastError());
@@ -595,9 +651,21 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
     return rrows;
   }
   dim3 grid(cdiv(M, bm), cdiv(cw.cout, bn), cw.phases);
-  std::snprintf(nm, sizeof nm, "igemm_f32_kernel<%d, %d, %d, %d>", bm, bn, epi == EPI_STATS ? src_mode : SRC_PLAIN,
-                epi);
+  if (x3) std::snprintf(nm, sizeof nm, "%s<%d, %d, %d>", kname, bm, bn, epi);
+  else std::snprintf(nm, sizeof nm, "%s<%d, %d, %d, %d>", kname, bm, bn, epi == EPI_STATS ? src_mode : SRC_PLAIN, epi);
   R.begin(nm, flops, bytes);
+  if (x3) {
+    switch (epi) {
+      case EPI_STATS: launch_x3_tiles<EPI_STATS>(bm, bn, xp, grid, R.st); break;
+      case EPI_BIAS: launch_x3_tiles<EPI_BIAS>(bm, bn, xp, grid, R.st); break;
+      case EPI_BIAS_GELU: launch_x3_tiles<EPI_BIAS_GELU>(bm, bn, xp, grid, R.st); break;
+      case EPI_BIAS_RES: launch_x3_tiles<EPI_BIAS_RES>(bm, bn, xp, grid, R.st); break;
+      default: throw Error(DMX_E_INTERNAL, "bad epilogue");
+    }
+    R.end();
+    HIPCHK(hipGetLastError());
+    return rrows;
+  }
   switch (epi) {
     case EPI_STATS:
       if (src_mode == SRC_NCHW) launch_ig_tiles<SRC_NCHW, EPI_STATS>(bm, bn, p, grid, R.st);
@@ -800,7 +868,7 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
     e.out = emb;
     R.layer = "embed";
     R.begin("embed_kernel", 2.0 * N * (24.0 * 256 + 256.0 * 256 + 256.0 * m->hsum), 4.0 * (256.0 * 256 + 256.0 * m->hsum));
-    embed_kernel<<<N, 256, 0, R.st>>>(e);
+    embed_kernel<<<dim3(N, cdiv(m->hsum, 256)), 256, 0, R.st>>>(e);
     R.end();
     R.tap("emb", emb, (size_t)N * m->hsum);
     HIPCHK(hipGetLastError());
@@ -1132,6 +1200,21 @@ int dmx_model_finalize(dmx_model* m, void* stream) {
 }
 
 int64_t dmx_model_workspace_bytes(const dmx_model* m) { return m ? (int64_t)m->ws_cap : -1; }
+
+int dmx_model_set_precision(dmx_model* m, int prec) {
+  return guarded([&] {
+    REQUIRE(m != nullptr, "null model");
+    REQUIRE(prec == 0 || prec == 1, "precision must be 0 (fp32 MFMA) or 1 (fp16x3 split)");
+    if (m->prec != prec && m->has_graph) {
+      (void)hipGraphExecDestroy(m->gexec);
+      (void)hipGraphDestroy(m->graph);
+      m->has_graph = false;
+    }
+    m->prec = prec;
+  });
+}
+
+int dmx_model_get_precision(const dmx_model* m) { return m ? m->prec : -1; }
 
 int dmx_debug_enable(dmx_model* m, int on) {
   return guarded([&] {

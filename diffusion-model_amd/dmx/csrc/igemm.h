@@ -48,6 +48,100 @@ struct IgemmParams {
 constexpr int IG_BK = 16;
 constexpr int IG_LDS_STRIDE = 20;  // floats per LDS row (16 + 4 pad)
 
+// Shared epilogue of the implicit GEMMs: accumulators (C/D layout of the 32x32 MFMA:
+// col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)) -> split-K slab | output (+bias,
+// GELU, residual) and GroupNorm partials.
+template <int BM, int BN, int EPI>
+DMX_DEV void igemm_epilogue(const IgemmParams& p, floatx16 (&acc)[BM / 64][BN / 64], int phase, int m0, int n0,
+                            int wm, int wn, int fr, int fh) {
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
+  const int HW = p.H * p.W;
+  if constexpr (EPI == EPI_PARTIAL) {
+    float* dst = p.partial + (size_t)blockIdx.z * p.M * p.Cout;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = n0 + wn * WN + j * 32 + fr;
+          if (m < p.M && col < p.Cout) dst[(size_t)m * p.Cout + col] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+  const int nseg = EPI == EPI_STATS ? p.Cout / p.seg : 1;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    float s1[TN], s2[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) s1[j] = s2[j] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * fh;
+      const int m = m0 + wm * WM + i * 32 + row;
+      const bool mv = m < p.M;
+      size_t oidx = 0;
+      int nn = 0, rr = 0;
+      if (mv) {
+        nn = m / HW;
+        rr = m - nn * HW;
+        const int y = rr / p.W, x = rr - y * p.W;
+        oidx = ((size_t)nn * p.Hout + (y * p.osy + p.py[phase])) * p.Wout + (x * p.osx + p.px[phase]);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * WN + j * 32 + fr;
+        const bool v = mv && col < p.Cout;
+        float val = acc[i][j][r];
+        if (p.bias != nullptr && col < p.Cout) val += p.bias[col];
+        if constexpr (EPI == EPI_BIAS_GELU) val = gelu(val);
+        if constexpr (EPI == EPI_BIAS_RES) {
+          if (v) val += p.res[oidx * p.Cout + col];
+        }
+        if (v) p.out[oidx * p.Cout + col] = val;
+        if constexpr (EPI == EPI_STATS) {
+          const float a1 = v ? val : 0.f;
+          if (p.rgrp == 32) {  // accumulate the lane's 16 rows, reduce across lanes below
+            s1[j] += a1;
+            s2[j] += a1 * a1;
+          } else {
+            float t1 = a1, t2 = a1 * a1;
+            for (int o = 1; o < p.seg; o <<= 1) {
+              t1 += __shfl_xor(t1, o, 64);
+              t2 += __shfl_xor(t2, o, 64);
+            }
+            const size_t er = ((size_t)nn * p.nphase + phase) * HW + rr;
+            if (v && (fr & (p.seg - 1)) == 0) p.rowpart[er * nseg + col / p.seg] = make_float2(t1, t2);
+          }
+        }
+      }
+    }
+    if constexpr (EPI == EPI_STATS) {
+      if (p.rgrp == 32) {
+        const int mb = m0 + wm * WM + i * 32;  // 32-row group, within one sample (HW % 32 == 0)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          float t1 = s1[j], t2 = s2[j];
+          for (int o = 1; o < p.seg; o <<= 1) {
+            t1 += __shfl_xor(t1, o, 64);
+            t2 += __shfl_xor(t2, o, 64);
+          }
+          t1 += __shfl_xor(t1, 32, 64);
+          t2 += __shfl_xor(t2, 32, 64);
+          const int col = n0 + wn * WN + j * 32 + fr;
+          if (mb < p.M && col < p.Cout && fh == 0 && (fr & (p.seg - 1)) == 0) {
+            const int nn = mb / HW, lg = (mb - nn * HW) / 32;
+            const size_t er = ((size_t)nn * p.nphase + phase) * (HW / 32) + lg;
+            p.rowpart[er * nseg + col / p.seg] = make_float2(t1, t2);
+          }
+        }
+      }
+    }
+  }
+}
+
 template <int BM, int BN, int SRC, int EPI>
 __global__ __launch_bounds__(256) void igemm_f32_kernel(const IgemmParams p) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
@@ -150,91 +244,7 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(const IgemmParams p) {
     __syncthreads();
   }
 
-  // ---- epilogue -------------------------------------------------------------
-  if constexpr (EPI == EPI_PARTIAL) {
-    float* dst = p.partial + (size_t)blockIdx.z * p.M * p.Cout;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int col = n0 + wn * WN + j * 32 + fr;
-          if (m < p.M && col < p.Cout) dst[(size_t)m * p.Cout + col] = acc[i][j][r];
-        }
-      }
-    return;
-  }
-  const int nseg = EPI == EPI_STATS ? p.Cout / p.seg : 1;
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    float s1[TN], s2[TN];
-#pragma unroll
-    for (int j = 0; j < TN; ++j) s1[j] = s2[j] = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * fh;
-      const int m = m0 + wm * WM + i * 32 + row;
-      const bool mv = m < p.M;
-      size_t oidx = 0;
-      int nn = 0, rr = 0;
-      if (mv) {
-        nn = m / HW;
-        rr = m - nn * HW;
-        const int y = rr / p.W, x = rr - y * p.W;
-        oidx = ((size_t)nn * p.Hout + (y * p.osy + p.py[phase])) * p.Wout + (x * p.osx + p.px[phase]);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = n0 + wn * WN + j * 32 + fr;
-        const bool v = mv && col < p.Cout;
-        float val = acc[i][j][r];
-        if (p.bias != nullptr && col < p.Cout) val += p.bias[col];
-        if constexpr (EPI == EPI_BIAS_GELU) val = gelu(val);
-        if constexpr (EPI == EPI_BIAS_RES) {
-          if (v) val += p.res[oidx * p.Cout + col];
-        }
-        if (v) p.out[oidx * p.Cout + col] = val;
-        if constexpr (EPI == EPI_STATS) {
-          const float a1 = v ? val : 0.f;
-          if (p.rgrp == 32) {  // accumulate the lane's 16 rows, reduce across lanes below
-            s1[j] += a1;
-            s2[j] += a1 * a1;
-          } else {
-            float t1 = a1, t2 = a1 * a1;
-            for (int o = 1; o < p.seg; o <<= 1) {
-              t1 += __shfl_xor(t1, o, 64);
-              t2 += __shfl_xor(t2, o, 64);
-            }
-            const size_t er = ((size_t)nn * p.nphase + phase) * HW + rr;
-            if (v && (fr & (p.seg - 1)) == 0) p.rowpart[er * nseg + col / p.seg] = make_float2(t1, t2);
-          }
-        }
-      }
-    }
-    if constexpr (EPI == EPI_STATS) {
-      if (p.rgrp == 32) {
-        const int mb = m0 + wm * WM + i * 32;  // 32-row group, within one sample (HW % 32 == 0)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          float t1 = s1[j], t2 = s2[j];
-          for (int o = 1; o < p.seg; o <<= 1) {
-            t1 += __shfl_xor(t1, o, 64);
-            t2 += __shfl_xor(t2, o, 64);
-          }
-          t1 += __shfl_xor(t1, 32, 64);
-          t2 += __shfl_xor(t2, 32, 64);
-          const int col = n0 + wn * WN + j * 32 + fr;
-          if (mb < p.M && col < p.Cout && fh == 0 && (fr & (p.seg - 1)) == 0) {
-            const int nn = mb / HW, lg = (mb - nn * HW) / 32;
-            const size_t er = ((size_t)nn * p.nphase + phase) * (HW / 32) + lg;
-            p.rowpart[er * nseg + col / p.seg] = make_float2(t1, t2);
-          }
-        }
-      }
-    }
-  }
+  igemm_epilogue<BM, BN, EPI>(p, acc, phase, m0, n0, wm, wn, fr, fh);
 }
 
 // Split-K reduction + the epilogue the GEMM would have applied (deterministic:

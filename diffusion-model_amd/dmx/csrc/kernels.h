@@ -40,8 +40,10 @@ struct EmbedParams {
   float* out;                  // [n][hsum]
 };
 
+// grid = (n, parts): every block recomputes the sample's 256-wide embedding (cheap) and
+// produces its 1/parts slice of the concatenated head outputs (coalesced weight reads).
 __global__ __launch_bounds__(256) void embed_kernel(const EmbedParams p) {
-  __shared__ float e[256], s[256], h[256], in24[24];
+  __shared__ float s[256], h[256], in24[24];
   const int n = blockIdx.x, k = threadIdx.x;
   int64_t t = p.t[(size_t)(p.t_mod ? n % p.t_mod : n) * p.t_stride];
   t = t < 1 ? 1 : (t > p.tmax ? p.tmax : t);
@@ -63,17 +65,30 @@ __global__ __launch_bounds__(256) void embed_kernel(const EmbedParams p) {
     for (int j = 0; j < 24; ++j) a += p.w0[k * 24 + j] * in24[j];
     h[k] = silu(a);
     __syncthreads();
-    float c = p.b2[k];
-    for (int j = 0; j < 256; ++j) c += p.w2t[j * 256 + k] * h[j];
-    v += c;
+    float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
+#pragma unroll 4
+    for (int j = 0; j < 256; j += 4) {
+      c0 += p.w2t[(j + 0) * 256 + k] * h[j + 0];
+      c1 += p.w2t[(j + 1) * 256 + k] * h[j + 1];
+      c2 += p.w2t[(j + 2) * 256 + k] * h[j + 2];
+      c3 += p.w2t[(j + 3) * 256 + k] * h[j + 3];
+    }
+    v += p.b2[k] + ((c0 + c1) + (c2 + c3));
   }
-  e[k] = v;
   s[k] = silu(v);
   __syncthreads();
-  for (int o = k; o < p.hsum; o += 256) {
-    float a = p.bh[o];
-    for (int j = 0; j < 256; ++j) a += p.wht[(size_t)j * p.hsum + o] * s[j];
-    p.out[(size_t)n * p.hsum + o] = a;
+  const int per = (p.hsum + gridDim.y - 1) / gridDim.y;
+  const int o = blockIdx.y * per + k;
+  if (k < per && o < p.hsum) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll 4
+    for (int j = 0; j < 256; j += 4) {
+      a0 += p.wht[(size_t)(j + 0) * p.hsum + o] * s[j + 0];
+      a1 += p.wht[(size_t)(j + 1) * p.hsum + o] * s[j + 1];
+      a2 += p.wht[(size_t)(j + 2) * p.hsum + o] * s[j + 2];
+      a3 += p.wht[(size_t)(j + 3) * p.hsum + o] * s[j + 3];
+    }
+    p.out[(size_t)n * p.hsum + o] = p.bh[o] + ((a0 + a1) + (a2 + a3));
   }
 }
 

@@ -6,6 +6,7 @@ moves pointers: torch provides device memory and streams.
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 from typing import Dict, Optional, Tuple
 
@@ -97,6 +98,22 @@ class NativeModel:
             check(self.lib.dmx_model_finalize(self.handle, ctypes.c_void_p(_stream(self.device))))
         del keep
         self._side_stream = None
+        env = os.environ.get("DMX_PRECISION")
+        if env:
+            self.set_precision(env)
+
+    PRECISIONS = {"fp32": 0, "x3": 1}
+
+    def set_precision(self, prec) -> None:
+        """GEMM arithmetic: "x3" (default; fp32 split into fp16 hi+lo, 3 MFMAs, fp32 accumulate)
+        or "fp32" (fp32 MFMA, exact fp32 products)."""
+        code = self.PRECISIONS[prec] if isinstance(prec, str) else int(prec)
+        check(self.lib.dmx_model_set_precision(self.handle, code))
+
+    @property
+    def precision(self) -> str:
+        code = self.lib.dmx_model_get_precision(self.handle)
+        return {v: k for k, v in self.PRECISIONS.items()}[code]
 
     def __del__(self):
         try:

@@ -69,6 +69,10 @@ int dmx_model_destroy(dmx_model* m);
 int dmx_model_set_tensor(dmx_model* m, const char* name, const float* dev_ptr, const int64_t* shape, int ndim);
 /* Repack every registered tensor into the model's kernel layouts (device-side). */
 int dmx_model_finalize(dmx_model* m, void* stream);
+/* GEMM arithmetic: 0 = fp32 MFMA (exact fp32 products), 1 (default) = fp32 operands split
+ * into fp16 hi+lo on the fp16 matrix cores (3 MFMAs, fp32 accumulate, ~1e-7 relative). */
+int dmx_model_set_precision(dmx_model* m, int prec);
+int dmx_model_get_precision(const dmx_model* m);
 
 /* ---- U-Net forward (replaces model(x, t, y, cond_vals, cond_mask), diff.py:149-150) --
  * x: (n,in_ch,h,w); t: (n,) int64 in [1, tmax]; y: (n,) int64 or NULL (DMX_UNET);

@@ -53,8 +53,18 @@ def test_library_is_native(cuda):
     assert isinstance(lib, ctypes.CDLL)
 
 
+@pytest.fixture(params=["x3", "fp32"])
+def prec(request, model):
+    """Both GEMM arithmetics: fp16 hi/lo x3 split (default) and fp32 MFMA."""
+    nm = model.native()
+    old = nm.precision
+    nm.set_precision(request.param)
+    yield request.param
+    nm.set_precision(old)
+
+
 @pytest.mark.parametrize("name", ["forward_32.npz", "forward_28.npz"])
-def test_unet_forward_golden(golden, model, cuda, name):
+def test_unet_forward_golden(golden, model, cuda, name, prec):
     g = golden(name)
     dev = lambda k: torch.from_numpy(g[k]).to(cuda)
     with torch.no_grad():
@@ -139,7 +149,7 @@ def test_ddpm_update_bit_exact(cuda):
     assert torch.equal(out2, ref.ddpm_update(x, eu, t, a, ab, nz, clamp_prev=False))
 
 
-def test_cfg_step_full_batch_vs_oracle(model, cuda, unet_sd):
+def test_cfg_step_full_batch_vs_oracle(model, cuda, unet_sd, prec):
     """One CFG step at the benchmark shape B=64, 32x32x4 (2B = 128 sample-forwards)."""
     import diff
     d = diff.Diffuser(1000, device=cuda)
@@ -161,7 +171,7 @@ def test_cfg_step_full_batch_vs_oracle(model, cuda, unet_sd):
     assert rel(out, exp) < TOL
 
 
-def test_trajectory_T1000_golden(golden, model, vae, cuda):
+def test_trajectory_T1000_golden(golden, model, vae, cuda, prec):
     """Full T=1000 CFG trajectory (B=2) on the reference's own draws: latents <= 1e-4, pixels +-1."""
     import diff
     g = golden("traj_T1000_B2.npz")
