@@ -4,6 +4,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -315,7 +316,7 @@ struct Packer {
     c.cin = cin_pad;
     c.cout = cout;
     c.taps = ks * ks;
-    c.kpad = rup(c.taps * cin_pad, X3_BK);
+    c.kpad = rup(c.taps * cin_pad, 64);
     c.npad = rup(cout, 128);
     c.B = alloc((size_t)c.npad * c.kpad);
     if (cin_pad == cin) {
@@ -338,7 +339,7 @@ struct Packer {
     c.cin = fin;
     c.cout = fout;
     c.taps = 1;
-    c.kpad = rup(fin, X3_BK);
+    c.kpad = rup(fin, 64);
     c.npad = rup(fout, 128);
     c.B = alloc((size_t)c.npad * c.kpad);
     repack(c.B, in(w).first, 1, 1, c.npad, c.kpad, fout, fin, 1);
@@ -352,7 +353,7 @@ struct Packer {
     c.cout = cout;
     c.taps = 4;
     c.phases = 4;
-    c.kpad = rup(4 * cin, X3_BK);
+    c.kpad = rup(4 * cin, 64);
     c.npad = rup(cout, 128);
     c.B = alloc((size_t)4 * c.npad * c.kpad);
     repack(c.B, in(w).first, 2, 4, c.npad, c.kpad, cout, cin, 4);
@@ -548,12 +549,46 @@ static void launch_ig_tiles(int bm, int bn, const IgemmParams& p, dim3 grid, hip
   else launch_ig<64, 64, SRC, EPI>(p, grid, st);
 }
 
+// Pipeline variant of the x3 GEMM (A/B experiments; DMX_X3_PIPE env: 0 = BK32 x 2 LDS buffers,
+// 1 = BK32 x 1 buffer, 2 = BK64 x 1 buffer).
+static int x3_pipe() {
+  static int v = [] {
+    const char* e = std::getenv("DMX_X3_PIPE");
+    return e ? std::atoi(e) : 2;
+  }();
+  return v;
+}
+
+// Mid-ResBlock activation emitted as fp16 hi/lo planes for the split GEMM (DMX_SPLIT_A=0 disables).
+static bool split_a_enabled() {
+  static bool v = [] {
+    const char* e = std::getenv("DMX_SPLIT_A");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
+template <int EPI, int BK, int NB, int SA>
+static void launch_x3_s(int bm, int bn, const X3Params& p, dim3 grid, hipStream_t st) {
+  if (bm == 128 && bn == 128) igemm_x3_kernel<128, 128, EPI, BK, NB, SA><<<grid, 256, 0, st>>>(p);
+  else if (bm == 128) igemm_x3_kernel<128, 64, EPI, BK, NB, SA><<<grid, 256, 0, st>>>(p);
+  else if (bn == 128) igemm_x3_kernel<64, 128, EPI, BK, NB, SA><<<grid, 256, 0, st>>>(p);
+  else igemm_x3_kernel<64, 64, EPI, BK, NB, SA><<<grid, 256, 0, st>>>(p);
+}
+
+template <int EPI, int BK, int NB>
+static void launch_x3_v(int bm, int bn, const X3Params& p, dim3 grid, hipStream_t st) {
+  if (p.Ash != nullptr) launch_x3_s<EPI, BK, NB, 1>(bm, bn, p, grid, st);
+  else launch_x3_s<EPI, BK, NB, 0>(bm, bn, p, grid, st);
+}
+
 template <int EPI>
 static void launch_x3_tiles(int bm, int bn, const X3Params& p, dim3 grid, hipStream_t st) {
-  if (bm == 128 && bn == 128) igemm_x3_kernel<128, 128, EPI><<<grid, 256, 0, st>>>(p);
-  else if (bm == 128) igemm_x3_kernel<128, 64, EPI><<<grid, 256, 0, st>>>(p);
-  else if (bn == 128) igemm_x3_kernel<64, 128, EPI><<<grid, 256, 0, st>>>(p);
-  else igemm_x3_kernel<64, 64, EPI><<<grid, 256, 0, st>>>(p);
+  switch (x3_pipe()) {
+    case 1: launch_x3_v<EPI, 32, 1>(bm, bn, p, grid, st); break;
+    case 2: launch_x3_v<EPI, 64, 1>(bm, bn, p, grid, st); break;
+    default: launch_x3_v<EPI, 32, 2>(bm, bn, p, grid, st); break;
+  }
 }
 
 // Implicit GEMM: conv3x3 (taps 9), ConvT phases (taps 4, phases 4), linear (taps 1).
@@ -561,7 +596,8 @@ static void launch_x3_tiles(int bm, int bn, const X3Params& p, dim3 grid, hipStr
 // 256 CUs are split along K into deterministic slabs reduced by splitk_reduce_kernel.
 // Returns the GroupNorm partial rows per sample it wrote (EPI_STATS).
 static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, const ConvW& cw, int epi, float* out,
-                const float* res, float2* rowpart, int seg) {
+                const float* res, float2* rowpart, int seg, const _Float16* ash = nullptr,
+                const _Float16* asl = nullptr) {
   const int M = N * H * W;
   if (cw.cout % 32 != 0) throw Error(DMX_E_INTERNAL, "gemm: Cout must be a multiple of 32");
   const int bn = (cw.cout % 128 == 0) ? 128 : 64;
@@ -569,7 +605,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   const int bm = tiles128 >= 512 ? 128 : 64;
   const int blocks = cdiv(M, bm) * cdiv(cw.cout, bn) * cw.phases;
   const bool x3 = R.m->prec == 1 && src_mode == SRC_PLAIN && cw.Bh != nullptr;
-  const int bk = x3 ? X3_BK : IG_BK;
+  const int bk = x3 ? (x3_pipe() == 2 ? 64 : X3_BK) : IG_BK;
   const int nkt = cw.kpad / bk;
   int splits = 1, ksplit = nkt;
   if (cw.phases == 1 && blocks < 256 && nkt * bk >= 512) {
@@ -588,20 +624,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   p.W = W;
   p.M = M;
   p.taps = cw.taps;
-  for (int ph = 0; ph < cw.phases; ++ph) {
-    for (int t = 0; t < cw.taps; ++t) {
-      if (cw.phases == 4) {
-        const int py = ph >> 1, px = ph & 1, jy = t >> 1, jx = t & 1;
-        p.dy[ph][t] = (int8_t)(py == 0 ? (jy == 0 ? 0 : -1) : (jy == 0 ? 1 : 0));
-        p.dx[ph][t] = (int8_t)(px == 0 ? (jx == 0 ? 0 : -1) : (jx == 0 ? 1 : 0));
-      } else if (cw.taps == 9) {
-        p.dy[ph][t] = (int8_t)(t / 3 - 1);
-        p.dx[ph][t] = (int8_t)(t % 3 - 1);
-      }
-    }
-    p.py[ph] = (int8_t)(cw.phases == 4 ? ph >> 1 : 0);
-    p.px[ph] = (int8_t)(cw.phases == 4 ? ph & 1 : 0);
-  }
+  p.geom = cw.phases == 4 ? 2 : (cw.taps == 9 ? 1 : 0);
   p.Kreal = cw.taps * cw.cin;
   p.Kpad = cw.kpad;
   p.Cout = cw.cout;
@@ -620,9 +643,12 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   p.rgrp = rgrp;
   p.nphase = cw.phases;
   if (s.C != cw.cin) throw Error(DMX_E_INTERNAL, "gemm: source channels != weight channels");
+  if (x3 && cw.cin < bk) throw Error(DMX_E_INTERNAL, "gemm: x3 path needs Cin >= K-step");
   if (src_mode != SRC_PLAIN && src_mode != SRC_NCHW) throw Error(DMX_E_INTERNAL, "gemm: unsupported source");
   X3Params xp;
   xp.g = p;
+  xp.Ash = ash;
+  xp.Asl = asl;
   xp.Bh = cw.Bh;
   xp.Bl = cw.Bl;
   xp.inv_scale = cw.inv_scale;
@@ -749,15 +775,24 @@ static float* resblock(Run& R, const ResW& w, const SrcDesc& in, int mode, int N
   const int seg = 32;
   float* r1 = R.ws.get<float>((size_t)M * w.mid);
   float2* rp1 = R.ws.get<float2>((size_t)M * (w.mid / seg));
-  float* a1 = R.ws.get<float>((size_t)M * w.mid);
+  const bool planes = R.m->prec == 1 && split_a_enabled() && w.c2.Bh != nullptr && w.mid >= 64;
+  float* a1 = R.ws.get<float>((size_t)M * w.mid);  // fp32 or, with planes, hi|lo f16 halves
   float* r2 = R.ws.get<float>((size_t)M * w.cout);
   float2* rp2 = R.ws.get<float2>((size_t)M * (w.cout / seg));
   float* out = R.ws.get<float>((size_t)M * w.cout);
   const int rr1 = gemm(R, in, mode, N, H, W, w.c1, EPI_STATS, r1, nullptr, rp1, seg);
   NormParams n1 = norm_params(r1, rp1, w.mid / seg, rr1, w.g1.p, w.b1.p, w.mid, HW, a1);
   n1.act = 1;
+  _Float16* a1h = reinterpret_cast<_Float16*>(a1);
+  _Float16* a1l = a1h + (size_t)M * w.mid;
+  if (planes) {
+    n1.out = nullptr;
+    n1.out_h = a1h;
+    n1.out_l = a1l;
+  }
   norm(R, n1, N);
-  const int rr2 = gemm(R, plain_src(a1, w.mid), SRC_PLAIN, N, H, W, w.c2, EPI_STATS, r2, nullptr, rp2, seg);
+  const int rr2 = gemm(R, plain_src(a1, w.mid), SRC_PLAIN, N, H, W, w.c2, EPI_STATS, r2, nullptr, rp2, seg,
+                       planes ? a1h : nullptr, planes ? a1l : nullptr);
   NormParams n2 = norm_params(r2, rp2, w.cout / seg, rr2, w.g2.p, w.b2.p, w.cout, HW, out);
   if (residual) {
     if (mode != SRC_PLAIN) throw Error(DMX_E_INTERNAL, "residual ResBlock needs a plain input");
@@ -789,6 +824,17 @@ static void layernorm(Run& R, const float* x, float* y, const Vec& w, const Vec&
 static void attention_core(Run& R, const float* qkv, float* out, int N, int L, int C) {
   if (R.plan) return;
   const int D = C / 4;
+  if (R.m->prec == 1) {
+    dim3 grid(cdiv(L, 128), 4, N);
+    R.begin("attention_x3_kernel<" + std::to_string(D) + ">", 4.0 * N * (double)L * L * C, 4.0 * (double)N * L * 4 * C);
+    if (D == 16) attention_x3_kernel<16><<<grid, 256, 0, R.st>>>(qkv, out, L, C);
+    else if (D == 32) attention_x3_kernel<32><<<grid, 256, 0, R.st>>>(qkv, out, L, C);
+    else if (D == 64) attention_x3_kernel<64><<<grid, 256, 0, R.st>>>(qkv, out, L, C);
+    else throw Error(DMX_E_INTERNAL, "attention: unsupported head dim");
+    R.end();
+    HIPCHK(hipGetLastError());
+    return;
+  }
   const int qt = L >= 256 ? 2 : 1;
   dim3 grid(cdiv(L, 64 * qt), 4, N);
   R.begin("attention_kernel<" + std::to_string(D) + ", " + std::to_string(qt) + ">", 4.0 * N * (double)L * L * C,

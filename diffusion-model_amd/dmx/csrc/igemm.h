@@ -27,12 +27,11 @@ struct IgemmParams {
   int H, W;           // GEMM row grid (input grid of the conv / token grid)
   int M;              // rows = N * H * W
   int taps;
-  int8_t dy[4][9], dx[4][9];  // tap offsets per phase
+  int geom;           // 0: linear (1 tap), 1: conv3x3 pad 1, 2: ConvTranspose 4x4/s2 phase (4 taps)
   int Kreal, Kpad;
   int Cout, Npad;
   int osy, osx;       // output stride (2 for ConvT phases)
   int Hout, Wout;
-  int8_t py[4], px[4];  // output offset per phase
   const float* Bw;    // [phases][Npad][Kpad]
   const float* bias;  // [Cout] or null
   float* out;         // NHWC [N][Hout][Wout][Cout]
@@ -46,6 +45,37 @@ struct IgemmParams {
 };
 
 constexpr int IG_BK = 16;
+
+// Input offset of `tap` (no memory lookups: a runtime-indexed kernarg table costs a global load
+// + vmcnt(0) per K-step, which drains the software pipeline).
+DMX_DEV void tap_offset(int geom, int phase, int tap, int& dy, int& dx) {
+  if (geom == 1) {
+    const int ty = (tap * 11) >> 5;  // tap / 3 for tap in [0, 8]
+    dy = ty - 1;
+    dx = tap - 3 * ty - 1;
+  } else if (geom == 2) {  // ConvT 4x4/s2/p1, output parity (py, px) = phase bits
+    const int jy = tap >> 1, jx = tap & 1;
+    dy = (phase >> 1) ? 1 - jy : -jy;
+    dx = (phase & 1) ? 1 - jx : -jx;
+  } else {
+    dy = dx = 0;
+  }
+}
+
+// XCD-aware tile order (cdna_hip_programming.md T1): hardware deals consecutive block ids
+// round-robin over the 8 XCDs; remap so every XCD walks a contiguous range of logical tiles
+// with the N tile fastest — the N tiles and the spatially neighbouring M tiles that re-read
+// the same input rows (3x3 taps) then share one L2.  Bijective for any grid size.
+DMX_DEV void xcd_tile(int& mt, int& nt, int& z) {
+  const int nm = gridDim.x, nn = gridDim.y;
+  const int total = nm * nn;
+  const int b = blockIdx.y * nm + blockIdx.x;  // dispatch order (x fastest)
+  const int xcd = b & 7, q = total >> 3, r = total & 7;
+  const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  mt = t / nn;
+  nt = t - mt * nn;
+  z = blockIdx.z;
+}
 constexpr int IG_LDS_STRIDE = 20;  // floats per LDS row (16 + 4 pad)
 
 // Shared epilogue of the implicit GEMMs: accumulators (C/D layout of the 32x32 MFMA:
@@ -88,7 +118,8 @@ DMX_DEV void igemm_epilogue(const IgemmParams& p, floatx16 (&acc)[BM / 64][BN / 
         nn = m / HW;
         rr = m - nn * HW;
         const int y = rr / p.W, x = rr - y * p.W;
-        oidx = ((size_t)nn * p.Hout + (y * p.osy + p.py[phase])) * p.Wout + (x * p.osx + p.px[phase]);
+        const int py = p.geom == 2 ? phase >> 1 : 0, px = p.geom == 2 ? phase & 1 : 0;
+        oidx = ((size_t)nn * p.Hout + (y * p.osy + py)) * p.Wout + (x * p.osx + px);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
@@ -153,8 +184,10 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(const IgemmParams p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int phase = EPI == EPI_PARTIAL ? 0 : blockIdx.z;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  int mt, nt, bz;
+  xcd_tile(mt, nt, bz);
+  const int phase = EPI == EPI_PARTIAL ? 0 : bz;
+  const int m0 = mt * BM, n0 = nt * BN;
   const int q = tid & 3;          // float4 piece within a 16-wide K slice
   const int rbase = tid >> 2;     // staging row (+ i * 64)
   const float* Bw = p.Bw + (size_t)phase * p.Npad * p.Kpad;
@@ -181,7 +214,8 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(const IgemmParams p) {
     const bool kv = k < p.Kreal;
     const int tap = kv ? k / C : 0;
     const int c = k - tap * C;
-    const int ddy = p.dy[phase][tap], ddx = p.dx[phase][tap];
+    int ddy, ddx;
+    tap_offset(p.geom, phase, tap, ddy, ddx);
 #pragma unroll
     for (int i = 0; i < AP; ++i) {
       const int iy = ay[i] + ddy, ix = ax[i] + ddx;

@@ -26,6 +26,8 @@ constexpr int X3_STRIDE = 40;  // f16 per LDS row (32 + 8 pad) = 80 bytes
 
 struct X3Params {
   IgemmParams g;           // geometry / epilogue (g.Bw unused)
+  const _Float16* Ash;     // SPLIT_A: activation hi / lo planes [N][H][W][C] (else g.src.src0 fp32)
+  const _Float16* Asl;
   const _Float16* Bh;      // [phases][Npad][Kpad] scaled hi
   const _Float16* Bl;      //                      scaled lo
   float inv_scale;         // 2^-e
@@ -40,61 +42,98 @@ DMX_DEV void split4(floatx4 v, half4& h, half4& l) {
   }
 }
 
-template <int BM, int BN, int EPI>
+template <int BM, int BN, int EPI, int BK = 32, int NBUF = 2, int SPLIT_A = 0>
 __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
   const IgemmParams& p = P.g;
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
-  constexpr int AP = BM * 8 / 256;   // float4 pieces of A per thread per K-step (8 per row)
-  constexpr int BP = BN * 4 / 256;   // 16-byte chunks of B per plane per thread (4 per row)
+  constexpr int RS = BK + 8;                 // f16 per LDS row (16-byte pad)
+  constexpr int APR = SPLIT_A ? BK / 8 : BK / 4;  // A pieces per row (8 f16 per plane | 4 fp32)
+  constexpr int BPR = BK / 8;                // 16-byte chunks per B row per plane
+  constexpr int AP = BM * APR / 256;
+  constexpr int BP = BN * BPR / 256;
+  constexpr int ARS = 256 / APR, BRS = 256 / BPR;  // rows covered per pass
   static_assert(TM >= 1 && TN >= 1 && AP >= 1 && BP >= 1, "tile");
 
-  __shared__ __attribute__((aligned(16))) _Float16 Ah[2][BM][X3_STRIDE];
-  __shared__ __attribute__((aligned(16))) _Float16 Al[2][BM][X3_STRIDE];
-  __shared__ __attribute__((aligned(16))) _Float16 Bhs[2][BN][X3_STRIDE];
-  __shared__ __attribute__((aligned(16))) _Float16 Bls[2][BN][X3_STRIDE];
+  __shared__ __attribute__((aligned(16))) _Float16 Ah[NBUF][BM][RS];
+  __shared__ __attribute__((aligned(16))) _Float16 Al[NBUF][BM][RS];
+  __shared__ __attribute__((aligned(16))) _Float16 Bhs[NBUF][BN][RS];
+  __shared__ __attribute__((aligned(16))) _Float16 Bls[NBUF][BN][RS];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int phase = EPI == EPI_PARTIAL ? 0 : blockIdx.z;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
-  const int qa = tid & 7, ra = tid >> 3;   // A: piece 0..7 of a row, row (+ i*32)
-  const int qb = tid & 3, rb = tid >> 2;   // B: chunk 0..3 of a row, row (+ i*64)
+  int mt, nt, bz;
+  xcd_tile(mt, nt, bz);
+  const int phase = EPI == EPI_PARTIAL ? 0 : bz;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int qa = tid % APR, ra = tid / APR;
+  constexpr int PW = SPLIT_A ? 8 : 4;  // channels per A piece
+  const int qb = tid % BPR, rb = tid / BPR;
   const size_t boff = (size_t)phase * p.Npad * p.Kpad;
   const _Float16* Bh = P.Bh + boff;
   const _Float16* Bl = P.Bl + boff;
   const int HW = p.H * p.W;
   const int C = p.src.C;
 
-  int an[AP], ay[AP], ax[AP];
-  bool av[AP];
+  // Per staged row: its pixel index (GEMM rows are input-grid pixels) and a bitmask of the
+  // taps whose input pixel is inside the map (zero padding / row validity).
+  int rpix[AP];
+  unsigned tmask[AP];
 #pragma unroll
   for (int i = 0; i < AP; ++i) {
-    const int m = m0 + ra + i * 32;
-    av[i] = m < p.M;
-    const int mm = av[i] ? m : 0;
-    an[i] = mm / HW;
-    const int r = mm - an[i] * HW;
-    ay[i] = r / p.W;
-    ax[i] = r - ay[i] * p.W;
+    const int m = m0 + ra + i * ARS;
+    rpix[i] = m < p.M ? m : 0;
+    unsigned mk = 0;
+    if (m < p.M) {
+      const int n = m / HW, r = m - n * HW, y = r / p.W, x = r - y * p.W;
+      for (int t = 0; t < p.taps; ++t) {
+        int dy, dx;
+        tap_offset(p.geom, phase, t, dy, dx);
+        if (y + dy >= 0 && y + dy < p.H && x + dx >= 0 && x + dx < p.W) mk |= 1u << t;
+      }
+    }
+    tmask[i] = mk;
   }
 
-  floatx4 ra4[AP];
+  floatx4 ra4[SPLIT_A ? 1 : AP];
+  half8 rah[SPLIT_A ? AP : 1], ral[SPLIT_A ? AP : 1];
   half8 rbh[BP], rbl[BP];
+  // (tap, channel) of this thread's A piece, advanced incrementally (C >= BK on this path)
+  int ltap = 0, lc = 0;
+  auto seek = [&](int kt) {
+    const int k = kt * BK + qa * PW;
+    ltap = k / C;
+    lc = k - ltap * C;
+  };
+  const float* __restrict__ asrc = p.src.src0;
   auto load_tile = [&](int kt) {
-    const int k = kt * X3_BK + qa * 4;
-    const bool kv = k < p.Kreal;
-    const int tap = kv ? k / C : 0;
-    const int c = k - tap * C;
-    const int ddy = p.dy[phase][tap], ddx = p.dx[phase][tap];
+    int ddy, ddx;
+    tap_offset(p.geom, phase, ltap, ddy, ddx);
+    const int delta = ddy * p.W + ddx;
+    const int tap = ltap, c = lc;
+    lc += BK;
+    if (lc >= C) {
+      lc -= C;
+      ++ltap;
+    }
 #pragma unroll
     for (int i = 0; i < AP; ++i) {
-      const int iy = ay[i] + ddy, ix = ax[i] + ddx;
-      const bool ok = kv && av[i] && iy >= 0 && ix >= 0 && iy < p.H && ix < p.W;
-      ra4[i] = ok ? ld4(p.src.src0 + (((size_t)an[i] * p.H + iy) * p.W + ix) * C + c) : floatx4{0.f, 0.f, 0.f, 0.f};
+      // unconditional load from a valid address, then select (no branch around the load)
+      const bool ok = (tmask[i] >> tap) & 1u;
+      const int off = ok ? (rpix[i] + delta) * C + c : 0;
+      if constexpr (SPLIT_A) {
+        const half8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+        const half8 h = *reinterpret_cast<const half8*>(P.Ash + off);
+        const half8 l = *reinterpret_cast<const half8*>(P.Asl + off);
+        rah[i] = ok ? h : z;
+        ral[i] = ok ? l : z;
+      } else {
+        const floatx4 v = ld4(asrc + off);
+        ra4[i] = ok ? v : floatx4{0.f, 0.f, 0.f, 0.f};
+      }
     }
 #pragma unroll
     for (int i = 0; i < BP; ++i) {
-      const size_t o = (size_t)(n0 + rb + i * 64) * p.Kpad + kt * X3_BK + qb * 8;
+      const size_t o = (size_t)(n0 + rb + i * BRS) * p.Kpad + kt * BK + qb * 8;
       rbh[i] = *reinterpret_cast<const half8*>(Bh + o);
       rbl[i] = *reinterpret_cast<const half8*>(Bl + o);
     }
@@ -102,15 +141,20 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
   auto store_tile = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < AP; ++i) {
-      half4 h, l;
-      split4(ra4[i], h, l);
-      *reinterpret_cast<half4*>(&Ah[buf][ra + i * 32][qa * 4]) = h;
-      *reinterpret_cast<half4*>(&Al[buf][ra + i * 32][qa * 4]) = l;
+      if constexpr (SPLIT_A) {
+        *reinterpret_cast<half8*>(&Ah[buf][ra + i * ARS][qa * 8]) = rah[i];
+        *reinterpret_cast<half8*>(&Al[buf][ra + i * ARS][qa * 8]) = ral[i];
+      } else {
+        half4 h, l;
+        split4(ra4[i], h, l);
+        *reinterpret_cast<half4*>(&Ah[buf][ra + i * ARS][qa * 4]) = h;
+        *reinterpret_cast<half4*>(&Al[buf][ra + i * ARS][qa * 4]) = l;
+      }
     }
 #pragma unroll
     for (int i = 0; i < BP; ++i) {
-      *reinterpret_cast<half8*>(&Bhs[buf][rb + i * 64][qb * 8]) = rbh[i];
-      *reinterpret_cast<half8*>(&Bls[buf][rb + i * 64][qb * 8]) = rbl[i];
+      *reinterpret_cast<half8*>(&Bhs[buf][rb + i * BRS][qb * 8]) = rbh[i];
+      *reinterpret_cast<half8*>(&Bls[buf][rb + i * BRS][qb * 8]) = rbl[i];
     }
   };
 
@@ -122,21 +166,10 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  int kbeg = 0, nK = p.Kpad / X3_BK;
-  if constexpr (EPI == EPI_PARTIAL) {
-    kbeg = blockIdx.z * p.ksplit;
-    nK = min(nK - kbeg, p.ksplit);
-  }
-  load_tile(kbeg);
-  store_tile(0);
-  __syncthreads();
-
   const int fr = lane & 31, fh = lane >> 5;
-  for (int kt = 0; kt < nK; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nK) load_tile(kbeg + kt + 1);
+  auto compute = [&](int buf) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < BK / 16; ++s) {
       half8 ah[TM], al[TM], bh[TN], bl[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -159,8 +192,34 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
         }
     }
-    if (kt + 1 < nK) store_tile(buf ^ 1);
+  };
+
+  int kbeg = 0, nK = p.Kpad / BK;
+  if constexpr (EPI == EPI_PARTIAL) {
+    kbeg = blockIdx.z * p.ksplit;
+    nK = min(nK - kbeg, p.ksplit);
+  }
+  seek(kbeg);
+  if constexpr (NBUF == 2) {
+    load_tile(kbeg);
+    store_tile(0);
     __syncthreads();
+    for (int kt = 0; kt < nK; ++kt) {
+      const int buf = kt & 1;
+      if (kt + 1 < nK) load_tile(kbeg + kt + 1);
+      compute(buf);
+      if (kt + 1 < nK) store_tile(buf ^ 1);
+      __syncthreads();
+    }
+  } else {
+    load_tile(kbeg);
+    for (int kt = 0; kt < nK; ++kt) {
+      store_tile(0);
+      __syncthreads();
+      if (kt + 1 < nK) load_tile(kbeg + kt + 1);  // in flight during the MFMAs
+      compute(0);
+      __syncthreads();
+    }
   }
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -188,6 +247,189 @@ __global__ void absmax_kernel(const float* src, size_t n, unsigned* out) {
     m = fmaxf(m, fabsf(src[i]));
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
   if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));  // non-negative floats order as uints
+}
+
+}  // namespace dmx
+
+namespace dmx {
+
+// ---------------------------------------------------------------------------
+// K5 multi-head attention core in split precision (fp32 values as fp16 hi+lo,
+// v_mfma_f32_32x32x16_f16, fp32 accumulate) — nn.MultiheadAttention(C, 4) inner product
+// softmax(q k^T / sqrt(D)) v (models/unet_cond.py:36,49).
+//
+// One wave = 32 queries; 64-key chunks staged in LDS (K as [key][d] hi/lo planes,
+// V transposed as [d][key] planes).  S^T = K Q^T (keys on rows, the wave's 32 queries on
+// lanes); softmax in the log2 domain (Q pre-scaled by log2(e)/sqrt(D)); then
+// O^T += V^T P^T where the S^T accumulator registers 8s..8s+7 are directly the B operand
+// of k-step s (row 16s + 8(j>>2) + 4h + (j&3) of the tile), and V^T is read with the same
+// key permutation.  D = 16 pads V^T to 32 rows (zero).
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(256) void attention_x3_kernel(const float* qkv, float* out, int L, int C) {
+  constexpr int KC = 64, KS = D + 8, VR = D < 32 ? 32 : D, VS = KC + 4, NKS = D / 16, NDT = VR / 32;
+  __shared__ __attribute__((aligned(16))) _Float16 Kh[KC][KS];
+  __shared__ __attribute__((aligned(16))) _Float16 Kl[KC][KS];
+  __shared__ __attribute__((aligned(16))) _Float16 Vh[VR][VS];
+  __shared__ __attribute__((aligned(16))) _Float16 Vl[VR][VS];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int hd = blockIdx.y, n = blockIdx.z;
+  const int fr = lane & 31, fh = lane >> 5;
+  const size_t rs = (size_t)3 * C;
+  const float* base = qkv + (size_t)n * L * rs;
+  const float qscale = 1.4426950408889634f / sqrtf((float)D);
+  const int q = blockIdx.x * 128 + wid * 32 + fr;
+
+  // Q^T fragments (B operand): lane (q, h) holds Q[q][16ks + 8h + j]
+  half8 qh[NKS], ql[NKS];
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    floatx4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+    if (q < L) {
+      const float* r = base + (size_t)q * rs + hd * D + 16 * ks + 8 * fh;
+      a = ld4(r);
+      b = ld4(r + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float va = a[j] * qscale, vb = b[j] * qscale;
+      const _Float16 ha = (_Float16)va, hb = (_Float16)vb;
+      qh[ks][j] = ha;
+      ql[ks][j] = (_Float16)(va - (float)ha);
+      qh[ks][j + 4] = hb;
+      ql[ks][j + 4] = (_Float16)(vb - (float)hb);
+    }
+  }
+  if constexpr (VR > D) {  // zero the padded V^T rows once
+    for (int i = tid; i < (VR - D) * VS; i += 256) {
+      Vh[D + i / VS][i % VS] = (_Float16)0.f;
+      Vl[D + i / VS][i % VS] = (_Float16)0.f;
+    }
+  }
+  floatx16 o[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+  float mrun = -INFINITY, lrun = 0.f;
+
+  for (int c0 = 0; c0 < L; c0 += KC) {
+    __syncthreads();  // previous chunk fully consumed
+    for (int i = tid; i < KC * (D / 4); i += 256) {
+      const int key = i / (D / 4), d4 = (i % (D / 4)) * 4;
+      floatx4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
+      if (c0 + key < L) {
+        const float* r = base + (size_t)(c0 + key) * rs + hd * D + d4;
+        kv = ld4(r + C);
+        vv = ld4(r + 2 * C);
+      }
+      half4 h, l;
+      split4(kv, h, l);
+      *reinterpret_cast<half4*>(&Kh[key][d4]) = h;
+      *reinterpret_cast<half4*>(&Kl[key][d4]) = l;
+      split4(vv, h, l);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        Vh[d4 + j][key] = h[j];
+        Vl[d4 + j][key] = l[j];
+      }
+    }
+    __syncthreads();
+    // S^T for the two 32-key tiles of the chunk
+    floatx16 sc[2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sc[kt][r] = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const half8 kh = *reinterpret_cast<const half8*>(&Kh[kt * 32 + fr][16 * ks + 8 * fh]);
+        const half8 kl = *reinterpret_cast<const half8*>(&Kl[kt * 32 + fr][16 * ks + 8 * fh]);
+        sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kl, qh[ks], sc[kt], 0, 0, 0);
+        sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, ql[ks], sc[kt], 0, 0, 0);
+        sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, qh[ks], sc[kt], 0, 0, 0);
+      }
+    }
+    // online softmax (log2 domain); lane holds keys (r&3)+8(r>>2)+4h of each tile
+    const int nvalid = L - c0;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+        if (key >= nvalid) sc[kt][r] = -INFINITY;
+        mx = fmaxf(mx, sc[kt][r]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mnew = fmaxf(mrun, mx);
+    const float alpha = exp2f(mrun - mnew);
+    mrun = mnew;
+    float ls = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float pv = exp2f(sc[kt][r] - mnew);
+        sc[kt][r] = pv;
+        ls += pv;
+      }
+    lrun = lrun * alpha + ls;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+    // O^T += V^T P^T
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        half8 ph, pl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float pv = sc[kt][8 * s + j];
+          const _Float16 h = (_Float16)pv;
+          ph[j] = h;
+          pl[j] = (_Float16)(pv - (float)h);
+        }
+        const int k0 = kt * 32 + 16 * s + 4 * fh;
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          const int d = dt * 32 + fr;
+          half8 vh, vl;
+          const half4 a0 = *reinterpret_cast<const half4*>(&Vh[d][k0]);
+          const half4 a1 = *reinterpret_cast<const half4*>(&Vh[d][k0 + 8]);
+          const half4 b0 = *reinterpret_cast<const half4*>(&Vl[d][k0]);
+          const half4 b1 = *reinterpret_cast<const half4*>(&Vl[d][k0 + 8]);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            vh[j] = a0[j];
+            vh[j + 4] = a1[j];
+            vl[j] = b0[j];
+            vl[j + 4] = b1[j];
+          }
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph, o[dt], 0, 0, 0);
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, pl, o[dt], 0, 0, 0);
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, o[dt], 0, 0, 0);
+        }
+      }
+  }
+  lrun += __shfl_xor(lrun, 32, 64);
+  const float inv = 1.0f / lrun;
+  if (q < L) {
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * fh;  // rows (r&3) + 8(r>>2) + 4h for r = 4g..4g+3
+        if (d < D) {
+          floatx4 v;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = o[dt][4 * g + j] * inv;
+          *reinterpret_cast<floatx4*>(out + ((size_t)n * L + q) * C + hd * D + d) = v;
+        }
+      }
+  }
 }
 
 }  // namespace dmx

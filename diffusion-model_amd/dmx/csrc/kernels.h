@@ -149,7 +149,8 @@ struct NormParams {
   int C, G, HW;
   const float* res; int act;
   const float* emb; int emb_stride; int emb_off;
-  float* out;
+  float* out;                      // fp32 output, or null when only the planes are written
+  _Float16* out_h; _Float16* out_l;  // optional fp16 hi/lo planes (split-precision GEMM operand)
 };
 
 __global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
@@ -208,7 +209,19 @@ __global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] += e[j];
     }
-    *reinterpret_cast<floatx4*>(p.out + off) = o;
+    if (p.out != nullptr) *reinterpret_cast<floatx4*>(p.out + off) = o;
+    if (p.out_h != nullptr) {
+      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+      h4 hh, ll;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const _Float16 h = (_Float16)o[j];
+        hh[j] = h;
+        ll[j] = (_Float16)(o[j] - (float)h);
+      }
+      *reinterpret_cast<h4*>(p.out_h + off) = hh;
+      *reinterpret_cast<h4*>(p.out_l + off) = ll;
+    }
   }
 }
 

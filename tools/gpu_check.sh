@@ -9,7 +9,7 @@ echo "[gpu_check] $(date) host=$(hostname)"; rocm-smi --showproductname 2>/dev/n
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
 echo "[gpu_check] smoke rc=$rc"; tail -3 gpurun_out/smoke.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 ${PYTEST_TIMEOUT:-900} python -m pytest tests -m gpu -q -rf --timeout=600 ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+timeout -k 10 ${PYTEST_TIMEOUT:-900} python -m pytest tests -m gpu -q -rf --timeout=600 ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 echo "[gpu_check] pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log
 ok $rc || exit $rc
 if [ -n "$BENCH" ]; then
