@@ -21,6 +21,9 @@ namespace dmx {
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 
+// 16 readable zero bytes: the load target of masked (padding) A pieces.
+__device__ __attribute__((aligned(16))) float g_zero16[4] = {0.f, 0.f, 0.f, 0.f};
+
 constexpr int X3_BK = 32;
 constexpr int X3_STRIDE = 40;  // f16 per LDS row (32 + 8 pad) = 80 bytes
 
@@ -40,6 +43,19 @@ DMX_DEV void split4(floatx4 v, half4& h, half4& l) {
     h[j] = hi;
     l[j] = (_Float16)(v[j] - (float)hi);
   }
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// hi/lo split of two fp32 values as packed f16 pairs: v_cvt_pk_f16_f32 (RNE), two
+// v_cvt_f32_f16, one v_pk_add_f32, v_cvt_pk_f16_f32 — 5 VALU ops per pair.
+DMX_DEV void split2(f32x2 v, unsigned& h, unsigned& l) {
+  const half2v hh = __builtin_convertvector(v, half2v);
+  const half2v ll = __builtin_convertvector(v - __builtin_convertvector(hh, f32x2), half2v);
+  h = __builtin_bit_cast(unsigned, hh);
+  l = __builtin_bit_cast(unsigned, ll);
 }
 
 template <int BM, int BN, int EPI, int BK = 32, int NBUF = 2, int SPLIT_A = 0>
@@ -117,18 +133,18 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
     }
 #pragma unroll
     for (int i = 0; i < AP; ++i) {
-      // unconditional load from a valid address, then select (no branch around the load)
+      // Padding taps / rows past M read 16 zero bytes from g_zero16: the select is on the
+      // ADDRESS, so nothing consumes the loaded data before store_tile and the loads stay
+      // in flight across compute() (a select on the data forced a vmcnt wait before the MFMAs).
       const bool ok = (tmask[i] >> tap) & 1u;
-      const int off = ok ? (rpix[i] + delta) * C + c : 0;
+      const int off = (rpix[i] + delta) * C + c;
       if constexpr (SPLIT_A) {
-        const half8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-        const half8 h = *reinterpret_cast<const half8*>(P.Ash + off);
-        const half8 l = *reinterpret_cast<const half8*>(P.Asl + off);
-        rah[i] = ok ? h : z;
-        ral[i] = ok ? l : z;
+        const _Float16* ph = ok ? P.Ash + off : reinterpret_cast<const _Float16*>(g_zero16);
+        const _Float16* pl = ok ? P.Asl + off : reinterpret_cast<const _Float16*>(g_zero16);
+        rah[i] = *reinterpret_cast<const half8*>(ph);
+        ral[i] = *reinterpret_cast<const half8*>(pl);
       } else {
-        const floatx4 v = ld4(asrc + off);
-        ra4[i] = ok ? v : floatx4{0.f, 0.f, 0.f, 0.f};
+        ra4[i] = ld4(ok ? asrc + off : g_zero16);
       }
     }
 #pragma unroll
@@ -300,10 +316,14 @@ __global__ __launch_bounds__(256) void attention_x3_kernel(const float* qkv, flo
       ql[ks][j + 4] = (_Float16)(vb - (float)hb);
     }
   }
-  if constexpr (VR > D) {  // zero the padded V^T rows once
+  // D < 32: V^T is padded to 32 rows; row D holds ones so O^T row D accumulates the
+  // softmax denominator on the matrix cores (rescaled by alpha with the rest of O).
+  constexpr bool ONES = VR > D;
+  if constexpr (ONES) {
     for (int i = tid; i < (VR - D) * VS; i += 256) {
-      Vh[D + i / VS][i % VS] = (_Float16)0.f;
-      Vl[D + i / VS][i % VS] = (_Float16)0.f;
+      const int r = D + i / VS;
+      Vh[r][i % VS] = (_Float16)(r == D ? 1.f : 0.f);
+      Vl[r][i % VS] = (_Float16)0.f;
     }
   }
   floatx16 o[NDT];
@@ -352,46 +372,60 @@ __global__ __launch_bounds__(256) void attention_x3_kernel(const float* qkv, flo
     }
     // online softmax (log2 domain); lane holds keys (r&3)+8(r>>2)+4h of each tile
     const int nvalid = L - c0;
-    float mx = -INFINITY;
+    if (nvalid < KC) {  // ragged last chunk only (uniform branch)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+          if (key >= nvalid) sc[kt][r] = -INFINITY;
+        }
+    }
+    float mx = sc[0][0];
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-        if (key >= nvalid) sc[kt][r] = -INFINITY;
-        mx = fmaxf(mx, sc[kt][r]);
-      }
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kt][r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mnew = fmaxf(mrun, mx);
-    const float alpha = exp2f(mrun - mnew);
+    const float alpha = __builtin_amdgcn_exp2f(mrun - mnew);  // exp2(-inf) = 0 on the first chunk
     mrun = mnew;
-    float ls = 0.f;
+    const f32x2 mn2 = {mnew, mnew}, al2 = {alpha, alpha};
+    f32x2 ls2 = {0.f, 0.f};
+    u32x4 phu[2][2], plu[2][2];  // P^T hi/lo fragments per (key tile, 16-key step)
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float pv = exp2f(sc[kt][r] - mnew);
-        sc[kt][r] = pv;
-        ls += pv;
-      }
-    lrun = lrun * alpha + ls;
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int jp = 0; jp < 4; ++jp) {
+          f32x2 v = {sc[kt][8 * s + 2 * jp], sc[kt][8 * s + 2 * jp + 1]};
+          v -= mn2;
+          v.x = __builtin_amdgcn_exp2f(v.x);
+          v.y = __builtin_amdgcn_exp2f(v.y);
+          if constexpr (!ONES) ls2 += v;
+          unsigned h, l;
+          split2(v, h, l);
+          phu[kt][s][jp] = h;
+          plu[kt][s][jp] = l;
+        }
+    if constexpr (!ONES) lrun = lrun * alpha + (ls2.x + ls2.y);
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+      for (int r = 0; r < 16; r += 2) {
+        f32x2 v = {o[dt][r], o[dt][r + 1]};
+        v *= al2;
+        o[dt][r] = v.x;
+        o[dt][r + 1] = v.y;
+      }
     // O^T += V^T P^T
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        half8 ph, pl;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float pv = sc[kt][8 * s + j];
-          const _Float16 h = (_Float16)pv;
-          ph[j] = h;
-          pl[j] = (_Float16)(pv - (float)h);
-        }
+        const half8 ph = __builtin_bit_cast(half8, phu[kt][s]);
+        const half8 pl = __builtin_bit_cast(half8, plu[kt][s]);
         const int k0 = kt * 32 + 16 * s + 4 * fh;
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt) {
@@ -414,7 +448,11 @@ __global__ __launch_bounds__(256) void attention_x3_kernel(const float* qkv, flo
         }
       }
   }
-  lrun += __shfl_xor(lrun, 32, 64);
+  if constexpr (ONES) {
+    lrun = __shfl(o[0][8], fr, 64);  // O^T row D = 16 lives in reg 8 of the h = 0 lane
+  } else {
+    lrun += __shfl_xor(lrun, 32, 64);
+  }
   const float inv = 1.0f / lrun;
   if (q < L) {
 #pragma unroll
