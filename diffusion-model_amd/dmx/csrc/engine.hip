@@ -16,6 +16,7 @@
 #include "igemm.h"
 #include "igemm_x3.h"
 #include "kernels.h"
+#include "tokmlp.h"
 
 namespace dmx {
 
@@ -849,9 +850,82 @@ static void attention_core(Run& R, const float* qkv, float* out, int N, int L, i
   HIPCHK(hipGetLastError());
 }
 
+static TokW tokw(const ConvW& c) { return TokW{c.Bh, c.Bl, c.bias, c.inv_scale, c.kpad}; }
+
+// Fused token kernels (tokmlp.h) for the x3 precision mode: TA -> attention core -> TB.
+static float* attn_block_fused(Run& R, const AttnW& a, const float* x, int N, int H, int W) {
+  const int C = a.c, M = N * H * W, L = H * W;
+  float* qkv = R.ws.get<float>((size_t)M * 3 * C);
+  float* ao = R.ws.get<float>((size_t)M * C);
+  float* out = R.ws.get<float>((size_t)M * C);
+  if (!R.plan) {
+    TokParams tp{};
+    tp.x = x;
+    tp.M = M;
+    tp.l1w = a.l1w.p;
+    tp.l1b = a.l1b.p;
+    tp.l2w = a.l2w.p;
+    tp.l2b = a.l2b.p;
+    const std::string cs = std::to_string(C);
+    tp.out = qkv;
+    tp.w0 = tokw(a.qkv);
+    const int nb = C == 64 ? 64 : 128;  // output columns per block (grid.y = 3C / nb)
+    const dim3 grid(cdiv(M, 64), 3 * C / nb);
+    R.begin("tok_ln_qkv_kernel<" + cs + ">", 2.0 * M * C * 3.0 * C, 16.0 * (double)M * C);
+    switch (C) {
+      case 64: tok_ln_qkv_kernel<64, 64><<<grid, 256, 0, R.st>>>(tp); break;
+      case 128: tok_ln_qkv_kernel<128, 128><<<grid, 256, 0, R.st>>>(tp); break;
+      default: tok_ln_qkv_kernel<256, 128><<<grid, 256, 0, R.st>>>(tp); break;
+    }
+    R.end();
+    HIPCHK(hipGetLastError());
+  }
+  attention_core(R, qkv, ao, N, L, C);
+  if (!R.plan) {
+    TokParams tp{};
+    tp.x = x;
+    tp.ao = ao;
+    tp.out = out;
+    tp.M = M;
+    tp.l1w = a.l1w.p;
+    tp.l1b = a.l1b.p;
+    tp.l2w = a.l2w.p;
+    tp.l2b = a.l2b.p;
+    tp.w0 = tokw(a.o);
+    tp.w1 = tokw(a.f1);
+    tp.w2 = tokw(a.f2);
+    // 32-token tiles when 64-token tiles would leave the chip under-filled (or C = 256)
+    const int tm = C == 64 ? 64 : (C == 256 || cdiv(M, 64) < 512) ? 32 : 64;
+    const int blocks = cdiv(M, tm);
+    R.begin("tok_attn_out_kernel<" + std::to_string(C) + ", " + std::to_string(tm) + ">", 6.0 * M * (double)C * C,
+            12.0 * (double)M * C);
+    if (C == 64) tok_attn_out_kernel<64, 64><<<blocks, 256, 0, R.st>>>(tp);
+    else if (C == 128 && tm == 64) tok_attn_out_kernel<128, 64><<<blocks, 256, 0, R.st>>>(tp);
+    else if (C == 128) tok_attn_out_kernel<128, 32><<<blocks, 256, 0, R.st>>>(tp);
+    else tok_attn_out_kernel<256, 32><<<blocks, 256, 0, R.st>>>(tp);
+    R.end();
+    HIPCHK(hipGetLastError());
+  }
+  R.tap(R.layer + ".qkv", qkv, (size_t)M * 3 * C);
+  R.tap(R.layer + ".ao", ao, (size_t)M * C);
+  R.tap(R.layer, out, (size_t)M * C);
+  return out;
+}
+
+static bool tok_fused_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DMX_TOK_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // AttenionBlock (models/unet_cond.py:32-52) on NHWC == (N, L, C) tokens.
 static float* attn_block(Run& R, const AttnW& a, const float* x, int N, int H, int W) {
   const int C = a.c, M = N * H * W, L = H * W;
+  if (R.m->prec == 1 && tok_fused_enabled() && (C == 64 || C == 128 || C == 256) && a.qkv.kpad == C &&
+      a.o.kpad == C && a.f1.kpad == C && a.f2.kpad == C)
+    return attn_block_fused(R, a, x, N, H, W);
   float* xl = R.ws.get<float>((size_t)M * C);
   float* qkv = R.ws.get<float>((size_t)M * 3 * C);
   float* ao = R.ws.get<float>((size_t)M * C);

@@ -1,0 +1,277 @@
+// dmx — fused per-token kernels of AttenionBlock (models/unet_cond.py:32-52), gfx950.
+//
+// The block is   xl = LN1(x);  av = MHA(xl) + xl;  out = FF(LN2(av)) + av
+// with FF = Linear -> GELU -> Linear.  Everything except the attention core is row-local
+// (one token = one row of C channels), so two kernels cover it with K = C resident:
+//
+//   tok_ln_qkv_kernel     qkv = LN1(x) Wqkv^T + b                      (TA)
+//   tok_attn_out_kernel   av  = ao Wo^T + bo + LN1(x)                   (TB, one kernel)
+//                         f   = GELU(LN2(av) W1^T + b1)
+//                         out = f W2^T + b2 + av
+//
+// replacing 2 LayerNorm + 4 GEMM launches and five (M, C) intermediates per block.
+//
+// Layout: one block = TM (64 | 32) tokens x all C channels (TA: x NB output columns),
+// 4 waves; the activation tile lives in LDS as f16 hi / lo planes [TM][C + 8] (row
+// stride ≡ 4 dwords mod 64 for C = 128/256 and 36 for C = 64: conflict-free ds_read_b128).  Weights are the
+// x3 B layout [Npad][Kpad] (scaled hi / lo), small and L2-resident, read straight into
+// MFMA B fragments (16 B per lane) with a rolling register prefetch — no LDS, no barrier.
+// Products are the x3 split (ah*bh + ah*bl + al*bh, fp32 accumulate) as in igemm_x3.h.
+#pragma once
+#include "common.h"
+#include "igemm_x3.h"
+
+namespace dmx {
+
+struct TokW {                 // one Linear in the x3 B layout
+  const _Float16* h;          // [Npad][Kpad] hi (scaled by 1/inv_scale)
+  const _Float16* l;          //               lo
+  const float* bias;          // [N]
+  float inv_scale;
+  int kpad;
+};
+
+struct TokParams {
+  const float* x;             // block input tokens [M][C] (NHWC rows)
+  const float* ao;            // TB: attention core output [M][C]
+  float* out;                 // TA: qkv [M][3C]; TB: block output [M][C]
+  const float* l1w;           // LN1 (AttenionBlock.ln)
+  const float* l1b;
+  const float* l2w;           // LN2 (ff_self[0])
+  const float* l2b;
+  TokW w0, w1, w2;            // TA: w0 = in_proj; TB: w0 = out_proj, w1 = ff_self[1], w2 = ff_self[3]
+  int M;
+};
+
+enum { ROWS_SPLIT = 0, ROWS_LN = 1, ROWS_STATS = 2 };
+
+// DPP lane exchange (no LDS round trip): quad_perm / row_half_mirror / row_mirror.
+template <int CTRL>
+DMX_DEV float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+// Sum over aligned groups of G lanes (G = 4, 8, 16); every lane of a group gets the same bits.
+template <int G>
+DMX_DEV float group_sum(float s) {
+  s += dpp_f<0xB1>(s);                          // quad_perm [1,0,3,2]
+  s += dpp_f<0x4E>(s);                          // quad_perm [2,3,0,1]
+  if constexpr (G >= 8) s += dpp_f<0x141>(s);   // row_half_mirror
+  if constexpr (G >= 16) s += dpp_f<0x140>(s);  // row_mirror
+  return s;
+}
+
+// TM rows (m0 .. m0+TM-1, zero past M) of an fp32 [.][ld] source -> A planes, either split
+// as-is (ROWS_SPLIT), LayerNorm'd then split (ROWS_LN), or only the LN statistics recorded
+// (ROWS_STATS).  A row is owned by G = C/16 lanes, 4 float4 each (columns 4g + 4Gj, so one
+// load instruction covers 16G contiguous bytes of a row); every load of the pass is issued
+// before any is used.  LN = nn.LayerNorm: two-pass mean / biased variance, eps 1e-5, the
+// same per-element expression as layernorm_kernel.
+template <int C, int TM, int MODE>
+DMX_DEV void tok_rows(const float* src, int ld, int m0, int M, const float* g, const float* b,
+                      _Float16 (*Ah)[C + 8], _Float16 (*Al)[C + 8], float* mu, float* rs) {
+  constexpr int G = C / 16, RP = 64 / G, RW = TM / 4, NP = RW / RP;
+  static_assert(G == 4 || G == 8 || G == 16, "C");
+  static_assert(NP >= 1 && RW % RP == 0, "rows per wave");
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int rr = lane / G, c0 = 4 * (lane % G);
+  floatx4 v[NP][4];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int m = min(m0 + wid * RW + p * RP + rr, M - 1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[p][j] = ld4(src + (size_t)m * ld + c0 + 4 * G * j);
+  }
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    const int row = wid * RW + p * RP + rr;
+    if (m0 + row >= M) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[p][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    if constexpr (MODE == ROWS_SPLIT) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        half4 h, l;
+        split4(v[p][j], h, l);
+        *reinterpret_cast<half4*>(&Ah[row][c0 + 4 * G * j]) = h;
+        *reinterpret_cast<half4*>(&Al[row][c0 + 4 * G * j]) = l;
+      }
+    } else {
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s += (v[p][j][0] + v[p][j][1]) + (v[p][j][2] + v[p][j][3]);
+      const float mean = group_sum<G>(s) / (float)C;
+      float q = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = v[p][j][e] - mean;
+          q += d * d;
+        }
+      const float rstd = 1.0f / sqrtf(group_sum<G>(q) / (float)C + 1e-5f);
+      if constexpr (MODE == ROWS_STATS) {
+        if (lane % G == 0) {
+          mu[row] = mean;
+          rs[row] = rstd;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = c0 + 4 * G * j;
+          const floatx4 gw = ld4(g + c), bw = ld4(b + c);
+          floatx4 y;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) y[e] = (v[p][j][e] - mean) * rstd * gw[e] + bw[e];
+          half4 h, l;
+          split4(y, h, l);
+          *reinterpret_cast<half4*>(&Ah[row][c]) = h;
+          *reinterpret_cast<half4*>(&Al[row][c]) = l;
+        }
+      }
+    }
+  }
+}
+
+// acc[j] = A[arow0 .. +32][0, C) . W[nw + 32j .. +32][0, C)^T  (x3 sum, still scaled by 2^e).
+// B fragments come straight from global memory (L2-resident weights) with a PD-step
+// rolling register prefetch.
+template <int C, int NT>
+DMX_DEV void tok_gemm(const _Float16 (*Ah)[C + 8], const _Float16 (*Al)[C + 8], const TokW& w, int nw,
+                      floatx16 (&acc)[NT], int arow0, int fr, int fh) {
+  constexpr int S = C / 16, PD = S < 4 ? S : 4;
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  const _Float16* wh = w.h + (size_t)(nw + fr) * w.kpad + 8 * fh;
+  const _Float16* wl = w.l + (size_t)(nw + fr) * w.kpad + 8 * fh;
+  const size_t jstride = (size_t)32 * w.kpad;
+  half8 bh[PD][NT], bl[PD][NT];
+  auto loadb = [&](int s, half8* h, half8* l) {
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      h[j] = *reinterpret_cast<const half8*>(wh + j * jstride + 16 * s);
+      l[j] = *reinterpret_cast<const half8*>(wl + j * jstride + 16 * s);
+    }
+  };
+#pragma unroll
+  for (int s = 0; s < PD; ++s) loadb(s, bh[s], bl[s]);
+  const int arow = arow0 + fr;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const half8 ah = *reinterpret_cast<const half8*>(&Ah[arow][16 * s + 8 * fh]);
+    const half8 al = *reinterpret_cast<const half8*>(&Al[arow][16 * s + 8 * fh]);
+    half8 ch[NT], cl[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      ch[j] = bh[s % PD][j];
+      cl[j] = bl[s % PD][j];
+    }
+    if (s + PD < S) loadb(s + PD, bh[s % PD], bl[s % PD]);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, ch[j], acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, cl[j], acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ch[j], acc[j], 0, 0, 0);
+    }
+  }
+}
+
+// Row of accumulator register r inside a wave's 32-row tile (v_mfma_f32_32x32x16 layout).
+DMX_DEV int tok_r(int fh, int r) { return (r & 3) + 8 * (r >> 2) + 4 * fh; }
+
+// TA: qkv = LN1(x) Wqkv^T + b_in (nn.MultiheadAttention in_proj on the LN1 output).
+// Block = 64 tokens x NB of the 3C output columns (grid.y = 3C / NB); waves 2 x 2.
+template <int C, int NB>
+__global__ __launch_bounds__(256) void tok_ln_qkv_kernel(const TokParams P) {
+  constexpr int NT = NB / 64;
+  __shared__ __attribute__((aligned(16))) _Float16 Ah[64][C + 8];
+  __shared__ __attribute__((aligned(16))) _Float16 Al[64][C + 8];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, fr = lane & 31, fh = lane >> 5;
+  const int wm = wid >> 1, wn = wid & 1, m0 = blockIdx.x * 64;
+  tok_rows<C, 64, ROWS_LN>(P.x, C, m0, P.M, P.l1w, P.l1b, Ah, Al, nullptr, nullptr);
+  __syncthreads();
+  const int nw = blockIdx.y * NB + wn * (NB / 2);
+  floatx16 acc[NT];
+  tok_gemm<C, NT>(Ah, Al, P.w0, nw, acc, wm * 32, fr, fh);
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int col = nw + 32 * j + fr;
+    const float bias = P.w0.bias[col];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wm * 32 + tok_r(fh, r);
+      if (m < P.M) P.out[(size_t)m * 3 * C + col] = acc[j][r] * P.w0.inv_scale + bias;
+    }
+  }
+}
+
+// TB: out-proj + residual, LN2, FF1 + GELU, FF2 + residual for TM tokens x all C channels.
+// TM = 64: waves 2 (rows) x 2 (cols); TM = 32: 1 x 4 (more blocks for small M / wide C).
+template <int C, int TM>
+__global__ __launch_bounds__(256) void tok_attn_out_kernel(const TokParams P) {
+  constexpr int WR = TM / 32, WC = 4 / WR, CW = C / WC, NT = CW / 32, VS = C + 4;
+  static_assert(NT >= 1, "tile");
+  __shared__ __attribute__((aligned(16))) _Float16 Ah[TM][C + 8];
+  __shared__ __attribute__((aligned(16))) _Float16 Al[TM][C + 8];
+  __shared__ __attribute__((aligned(16))) float Av[TM][VS];
+  __shared__ float mu1[TM], rs1[TM];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, fr = lane & 31, fh = lane >> 5;
+  const int wm = wid / WC, wn = wid % WC, m0 = blockIdx.x * TM;
+  const int M = P.M, nw = wn * CW, arow0 = wm * 32;
+
+  tok_rows<C, TM, ROWS_SPLIT>(P.ao, C, m0, M, nullptr, nullptr, Ah, Al, nullptr, nullptr);
+  tok_rows<C, TM, ROWS_STATS>(P.x, C, m0, M, nullptr, nullptr, Ah, Al, mu1, rs1);
+  __syncthreads();
+
+  floatx16 acc[NT];
+  // av = ao Wo^T + bo + LN1(x)   (models/unet_cond.py:49-50)
+  tok_gemm<C, NT>(Ah, Al, P.w0, nw, acc, arow0, fr, fh);
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int col = nw + 32 * j + fr;
+    const float bo = P.w0.bias[col], g1 = P.l1w[col], b1 = P.l1b[col];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = arow0 + tok_r(fh, r), m = min(m0 + row, M - 1);
+      const float xl = (P.x[(size_t)m * C + col] - mu1[row]) * rs1[row] * g1 + b1;
+      Av[row][col] = (acc[j][r] * P.w0.inv_scale + bo) + xl;
+    }
+  }
+  __syncthreads();
+  // LN2(av) -> A planes (ff_self[0])
+  tok_rows<C, TM, ROWS_LN>(&Av[0][0], VS, 0, TM, P.l2w, P.l2b, Ah, Al, nullptr, nullptr);
+  __syncthreads();
+  // f = GELU(LN2(av) W1^T + b1)  (ff_self[1:3])
+  tok_gemm<C, NT>(Ah, Al, P.w1, nw, acc, arow0, fr, fh);
+  __syncthreads();  // every wave is done reading the LN2 planes
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int col = nw + 32 * j + fr;
+    const float b = P.w1.bias[col];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = arow0 + tok_r(fh, r);
+      const float f = gelu(acc[j][r] * P.w1.inv_scale + b);
+      const _Float16 h = (_Float16)f;
+      Ah[row][col] = h;
+      Al[row][col] = (_Float16)(f - (float)h);
+    }
+  }
+  __syncthreads();
+  // out = f W2^T + b2 + av  (ff_self[3] + residual, models/unet_cond.py:51)
+  tok_gemm<C, NT>(Ah, Al, P.w2, nw, acc, arow0, fr, fh);
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int col = nw + 32 * j + fr;
+    const float b = P.w2.bias[col];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = arow0 + tok_r(fh, r), m = m0 + row;
+      if (m < M) P.out[(size_t)m * C + col] = (acc[j][r] * P.w2.inv_scale + b) + Av[row][col];
+    }
+  }
+}
+
+}  // namespace dmx
