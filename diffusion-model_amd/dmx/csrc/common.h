@@ -17,6 +17,19 @@ namespace dmx {
 DMX_DEV float gelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f)); }
 DMX_DEV float silu(float x) { return x / (1.0f + expf(-x)); }
 
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+
+// fp32 -> f16 hi + f16 lo (split-precision operand; lo = f16(v - hi) is exact to ~2^-22 |v|)
+DMX_DEV void split4(floatx4 v, half4& h, half4& l) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const _Float16 hi = (_Float16)v[j];
+    h[j] = hi;
+    l[j] = (_Float16)(v[j] - (float)hi);
+  }
+}
+
 // Input-source modes of a convolution / token GEMM (how the A operand's
 // element (n, iy, ix, c) is produced from HBM).
 enum SrcMode : int {

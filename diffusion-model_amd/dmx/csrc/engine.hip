@@ -721,8 +721,9 @@ static void gn_finalize(Run& R, const float2* rowpart, float2* stats, int N, int
 // or precomputed (stats).
 static void norm(Run& R, NormParams np, int N) {
   if (R.plan) return;
-  const size_t per = (size_t)np.HW * (np.C / 4);
-  const int chunks = (int)std::max<size_t>(1, std::min<size_t>(cdiv((int)per, 1024), cdiv(2048, N)));
+  // ~2048+ blocks in total, 256..1024 float4 per block (chunks are rounded up to 256 in-kernel)
+  const int per = np.HW * (np.C / 4);
+  const int chunks = std::max(1, std::min(cdiv(per, 256), std::max(cdiv(per, 1024), cdiv(2048, N))));
   R.begin("norm_kernel", 0.0, 4.0 * (double)N * np.HW * np.C * (np.res ? 3 : 2));
   norm_kernel<<<dim3(chunks, N), 256, 0, R.st>>>(np);
   R.end();

@@ -18,8 +18,6 @@
 
 namespace dmx {
 
-typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 
 // 16 readable zero bytes: the load target of masked (padding) A pieces.
 __device__ __attribute__((aligned(16))) float g_zero16[4] = {0.f, 0.f, 0.f, 0.f};
@@ -36,14 +34,6 @@ struct X3Params {
   float inv_scale;         // 2^-e
 };
 
-DMX_DEV void split4(floatx4 v, half4& h, half4& l) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const _Float16 hi = (_Float16)v[j];
-    h[j] = hi;
-    l[j] = (_Float16)(v[j] - (float)hi);
-  }
-}
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 half2v __attribute__((ext_vector_type(2)));
@@ -333,21 +323,33 @@ __global__ __launch_bounds__(256) void attention_x3_kernel(const float* qkv, flo
     for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
   float mrun = -INFINITY, lrun = 0.f;
 
+  // K/V chunk staging, software-pipelined: chunk c+1 is loaded into registers while chunk c
+  // is computed, then split into the LDS planes after the barrier.
+  constexpr int IT = KC * (D / 4) / 256;  // float4 of K (and of V) per thread per chunk
+  static_assert(IT >= 1 && KC * (D / 4) % 256 == 0, "staging");
+  floatx4 kr[IT], vr[IT];
+  auto load_kv = [&](int c0) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int i = tid + 256 * it, key = i / (D / 4), d4 = (i % (D / 4)) * 4;
+      const float* r = base + (size_t)min(c0 + key, L - 1) * rs + hd * D + d4;  // clamped: finite
+      kr[it] = ld4(r + C);
+      vr[it] = ld4(r + 2 * C);
+    }
+  };
+  load_kv(0);
   for (int c0 = 0; c0 < L; c0 += KC) {
     __syncthreads();  // previous chunk fully consumed
-    for (int i = tid; i < KC * (D / 4); i += 256) {
-      const int key = i / (D / 4), d4 = (i % (D / 4)) * 4;
-      floatx4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
-      if (c0 + key < L) {
-        const float* r = base + (size_t)(c0 + key) * rs + hd * D + d4;
-        kv = ld4(r + C);
-        vv = ld4(r + 2 * C);
-      }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int i = tid + 256 * it, key = i / (D / 4), d4 = (i % (D / 4)) * 4;
+      const bool kvalid = c0 + key < L;  // keys past L: zero K / V (their scores are masked)
+      const floatx4 z = {0.f, 0.f, 0.f, 0.f};
       half4 h, l;
-      split4(kv, h, l);
+      split4(kvalid ? kr[it] : z, h, l);
       *reinterpret_cast<half4*>(&Kh[key][d4]) = h;
       *reinterpret_cast<half4*>(&Kl[key][d4]) = l;
-      split4(vv, h, l);
+      split4(kvalid ? vr[it] : z, h, l);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         Vh[d4 + j][key] = h[j];
@@ -355,6 +357,7 @@ __global__ __launch_bounds__(256) void attention_x3_kernel(const float* qkv, flo
       }
     }
     __syncthreads();
+    if (c0 + KC < L) load_kv(c0 + KC);  // in flight during this chunk's MFMAs
     // S^T for the two 32-key tiles of the chunk
     floatx16 sc[2];
 #pragma unroll

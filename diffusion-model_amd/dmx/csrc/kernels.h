@@ -154,73 +154,85 @@ struct NormParams {
 };
 
 __global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
-  const int n = blockIdx.y;
-  __shared__ double r1[256], r2[256];
+  const int n = blockIdx.y, tid = threadIdx.x;
+  __shared__ double r1[4], r2[4];
   __shared__ float2 st_s;
-  if (p.rowpart != nullptr) {
+  if (p.rowpart != nullptr) {  // GroupNorm(1, C): reduce this sample's (sum, sumsq) partials in double
     const int cnt = p.rrows * p.nseg;
     const float2* rp = p.rowpart + (size_t)n * cnt;
     double s1 = 0.0, s2 = 0.0;
-    for (int i = threadIdx.x; i < cnt; i += 256) {
+    for (int i = tid; i < cnt; i += 256) {
       const float2 v = rp[i];
       s1 += (double)v.x;
       s2 += (double)v.y;
     }
-    r1[threadIdx.x] = s1;
-    r2[threadIdx.x] = s2;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if (threadIdx.x < o) {
-        r1[threadIdx.x] += r1[threadIdx.x + o];
-        r2[threadIdx.x] += r2[threadIdx.x + o];
-      }
-      __syncthreads();
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      s1 += __shfl_xor(s1, o, 64);
+      s2 += __shfl_xor(s2, o, 64);
     }
-    if (threadIdx.x == 0) {
+    if ((tid & 63) == 0) {
+      r1[tid >> 6] = s1;
+      r2[tid >> 6] = s2;
+    }
+    __syncthreads();
+    if (tid == 0) {
       const double cntd = (double)p.HW * (double)p.C;
-      const double mean = r1[0] / cntd;
-      double var = r2[0] / cntd - mean * mean;
+      const double mean = ((r1[0] + r1[1]) + (r1[2] + r1[3])) / cntd;
+      double var = ((r2[0] + r2[1]) + (r2[2] + r2[3])) / cntd - mean * mean;
       var = var < 0.0 ? 0.0 : var;
       st_s = make_float2((float)mean, (float)(1.0 / sqrt(var + 1e-5)));
     }
     __syncthreads();
   }
-  const int C4 = p.C / 4;
-  const size_t per = (size_t)p.HW * C4;
-  const size_t chunk = (per + gridDim.x - 1) / gridDim.x;
-  const size_t beg = blockIdx.x * chunk, end = min(per, beg + chunk);
-  const size_t base = (size_t)n * p.HW * p.C;
+  // This block's float4 range [beg, end) of the sample; chunks are multiples of 256, so when
+  // C/4 divides 256 a thread's channel is loop-invariant.  4 float4 per thread per pass,
+  // every load issued before any is used.
+  const int C4 = p.C >> 2;
+  const int per = p.HW * C4;
+  const int chunk = (((per + (int)gridDim.x - 1) / (int)gridDim.x) + 255) & ~255;
+  const int beg = blockIdx.x * chunk, end = min(per, beg + chunk);
+  const size_t base = (size_t)n * per * 4;
+  const float* raw = p.raw + base;
+  const float* res = p.res != nullptr ? p.res + base : nullptr;
   const int cpg = p.C / p.G;
-  for (size_t i = beg + threadIdx.x; i < end; i += 256) {
-    const int c = (int)(i % C4) * 4;
-    const size_t off = base + i * 4;
-    const float2 st = p.rowpart != nullptr ? st_s : p.stats[n * p.G + c / cpg];
-    floatx4 o = gn_apply4(ld4(p.raw + off), st, p.gamma, p.beta, c, 0);
-    if (p.res != nullptr) {
-      const floatx4 r = ld4(p.res + off);
+  const bool cfix = (256 % C4) == 0;
+  const int cthr = (tid % C4) * 4;
+  for (int i0 = beg + tid; i0 < end; i0 += 1024) {
+    floatx4 v[4], r[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = gelu(r[j] + o[j]);
-    } else if (p.act) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = gelu(o[j]);
+    for (int k = 0; k < 4; ++k) {
+      const int idx = min(i0 + 256 * k, end - 1);
+      v[k] = ld4(raw + (size_t)idx * 4);
+      if (res != nullptr) r[k] = ld4(res + (size_t)idx * 4);
     }
-    if (p.emb != nullptr) {
-      const floatx4 e = ld4(p.emb + (size_t)n * p.emb_stride + p.emb_off + c);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] += e[j];
-    }
-    if (p.out != nullptr) *reinterpret_cast<floatx4*>(p.out + off) = o;
-    if (p.out_h != nullptr) {
-      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-      h4 hh, ll;
+    for (int k = 0; k < 4; ++k) {
+      const int idx = i0 + 256 * k;
+      if (idx >= end) break;
+      const int c = cfix ? cthr : (idx % C4) * 4;
+      const float2 st = p.rowpart != nullptr ? st_s : p.stats[n * p.G + c / cpg];
+      floatx4 o = gn_apply4(v[k], st, p.gamma, p.beta, c, 0);
+      if (res != nullptr) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const _Float16 h = (_Float16)o[j];
-        hh[j] = h;
-        ll[j] = (_Float16)(o[j] - (float)h);
+        for (int j = 0; j < 4; ++j) o[j] = gelu(r[k][j] + o[j]);
+      } else if (p.act) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = gelu(o[j]);
       }
-      *reinterpret_cast<h4*>(p.out_h + off) = hh;
-      *reinterpret_cast<h4*>(p.out_l + off) = ll;
+      if (p.emb != nullptr) {
+        const floatx4 e = ld4(p.emb + (size_t)n * p.emb_stride + p.emb_off + c);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] += e[j];
+      }
+      const size_t off = base + (size_t)idx * 4;
+      if (p.out != nullptr) *reinterpret_cast<floatx4*>(p.out + off) = o;
+      if (p.out_h != nullptr) {
+        half4 hh, ll;
+        split4(o, hh, ll);
+        *reinterpret_cast<half4*>(p.out_h + off) = hh;
+        *reinterpret_cast<half4*>(p.out_l + off) = ll;
+      }
     }
   }
 }
