@@ -62,7 +62,7 @@ struct SrcDesc {
   int padT, padL;          // UPCAT: F.pad offsets of the upsampled map
   int act;                 // GNACT: 1 => apply GELU after the affine
   float scale;             // NCHW: divide by scale (VAE z / 0.18215), 1 => identity
-  int n_mod;               // NCHW: sample index taken modulo n_mod (CFG: both halves read x)
+  int n_mod;               // NCHW / UPCAT skip: sample index taken modulo n_mod (CFG: halves share it)
 };
 
 }  // namespace dmx

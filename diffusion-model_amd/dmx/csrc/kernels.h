@@ -149,17 +149,19 @@ struct NormParams {
   int C, G, HW;
   const float* res; int act;
   const float* emb; int emb_stride; int emb_off;
+  int n_src;                       // >0: raw / stats / res of output sample n come from sample n % n_src
   float* out;                      // fp32 output, or null when only the planes are written
   _Float16* out_h; _Float16* out_l;  // optional fp16 hi/lo planes (split-precision GEMM operand)
 };
 
 __global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
   const int n = blockIdx.y, tid = threadIdx.x;
+  const int ns = p.n_src > 0 ? n % p.n_src : n;  // source sample (CFG-shared trunk prefix)
   __shared__ double r1[4], r2[4];
   __shared__ float2 st_s;
   if (p.rowpart != nullptr) {  // GroupNorm(1, C): reduce this sample's (sum, sumsq) partials in double
     const int cnt = p.rrows * p.nseg;
-    const float2* rp = p.rowpart + (size_t)n * cnt;
+    const float2* rp = p.rowpart + (size_t)ns * cnt;
     double s1 = 0.0, s2 = 0.0;
     for (int i = tid; i < cnt; i += 256) {
       const float2 v = rp[i];
@@ -192,9 +194,9 @@ __global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
   const int per = p.HW * C4;
   const int chunk = (((per + (int)gridDim.x - 1) / (int)gridDim.x) + 255) & ~255;
   const int beg = blockIdx.x * chunk, end = min(per, beg + chunk);
-  const size_t base = (size_t)n * per * 4;
-  const float* raw = p.raw + base;
-  const float* res = p.res != nullptr ? p.res + base : nullptr;
+  const size_t base = (size_t)n * per * 4, sbase = (size_t)ns * per * 4;
+  const float* raw = p.raw + sbase;
+  const float* res = p.res != nullptr ? p.res + sbase : nullptr;
   const int cpg = p.C / p.G;
   const bool cfix = (256 % C4) == 0;
   const int cthr = (tid % C4) * 4;
@@ -211,7 +213,7 @@ __global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
       const int idx = i0 + 256 * k;
       if (idx >= end) break;
       const int c = cfix ? cthr : (idx % C4) * 4;
-      const float2 st = p.rowpart != nullptr ? st_s : p.stats[n * p.G + c / cpg];
+      const float2 st = p.rowpart != nullptr ? st_s : p.stats[ns * p.G + c / cpg];
       floatx4 o = gn_apply4(v[k], st, p.gamma, p.beta, c, 0);
       if (res != nullptr) {
 #pragma unroll

@@ -58,7 +58,10 @@ DMX_DEV floatx4 load_src4(const SrcDesc& s, int n, int iy, int ix, int c, int H,
     for (int j = 0; j < 4; ++j) o[j] = fmaxf(fmaxf(a[j], bb[j]), fmaxf(cc[j], d[j]));
     return o;
   } else if constexpr (SRC == SRC_UPCAT) {
-    if (c < s.C0) return ld4(s.src0 + (((size_t)n * H + iy) * W + ix) * s.C0 + c);
+    if (c < s.C0) {  // skip: sample n % n_mod when it was computed once for both CFG halves
+      const int ns = s.n_mod ? n % s.n_mod : n;
+      return ld4(s.src0 + (((size_t)ns * H + iy) * W + ix) * s.C0 + c);
+    }
     const int uy = iy - s.padT, ux = ix - s.padL;
     if (uy < 0 || ux < 0 || uy >= 2 * s.Hs || ux >= 2 * s.Ws) return floatx4{0.f, 0.f, 0.f, 0.f};
     return upsample4(s.src1, n, s.Hs, s.Ws, s.C - s.C0, uy, ux, c - s.C0);
