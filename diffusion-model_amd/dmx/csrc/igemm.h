@@ -66,6 +66,26 @@ DMX_DEV void tap_offset(int geom, int phase, int tap, int& dy, int& dx) {
 // round-robin over the 8 XCDs; remap so every XCD walks a contiguous range of logical tiles
 // with the N tile fastest — the N tiles and the spatially neighbouring M tiles that re-read
 // the same input rows (3x3 taps) then share one L2.  Bijective for any grid size.
+// Bitmask of the taps whose input pixel of output row m is inside the H x W map
+// (bit t = tap t of the GEMM geometry; 0 for m >= M).
+DMX_DEV unsigned tap_mask(int geom, int phase, int taps, int m, int M, int H, int W) {
+  if (m >= M) return 0u;
+  if (geom == 0) return 1u;
+  const int HW = H * W, n = m / HW, r = m - n * HW, y = r / W, x = r - y * W;
+  if (geom == 1) {  // 3x3, pad 1: outer product of row / column validity
+    const unsigned ry = (y > 0 ? 1u : 0u) | 2u | (y < H - 1 ? 4u : 0u);
+    const unsigned cx = (x > 0 ? 1u : 0u) | 2u | (x < W - 1 ? 4u : 0u);
+    return ((ry & 1u) ? cx : 0u) | ((ry & 2u) ? cx << 3 : 0u) | ((ry & 4u) ? cx << 6 : 0u);
+  }
+  unsigned mk = 0;
+  for (int t = 0; t < taps; ++t) {
+    int dy, dx;
+    tap_offset(geom, phase, t, dy, dx);
+    if (y + dy >= 0 && y + dy < H && x + dx >= 0 && x + dx < W) mk |= 1u << t;
+  }
+  return mk;
+}
+
 DMX_DEV void xcd_tile(int& mt, int& nt, int& z) {
   const int nm = gridDim.x, nn = gridDim.y;
   const int total = nm * nn;
@@ -102,6 +122,64 @@ DMX_DEV void igemm_epilogue(const IgemmParams& p, floatx16 (&acc)[BM / 64][BN / 
     return;
   }
   const int nseg = EPI == EPI_STATS ? p.Cout / p.seg : 1;
+  const bool strided = p.geom == 2;  // ConvT phases scatter rows; otherwise output row = m
+  float bj[TN];                      // bias of this lane's columns, loaded once
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn * WN + j * 32 + fr;
+    bj[j] = (p.bias != nullptr && col < p.Cout) ? p.bias[col] : 0.f;
+  }
+  if (!strided && (EPI != EPI_STATS || p.rgrp == 32)) {
+    // common case: output row = m, GroupNorm partials per 32-row group (no index divisions)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      float s1[TN], s2[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) s1[j] = s2[j] = 0.f;
+      const int mb = m0 + wm * WM + i * 32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mb + (r & 3) + 8 * (r >> 2) + 4 * fh;
+        const bool mv = m < p.M;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = n0 + wn * WN + j * 32 + fr;
+          const bool v = mv && col < p.Cout;
+          float val = acc[i][j][r] + bj[j];
+          if constexpr (EPI == EPI_BIAS_GELU) val = gelu(val);
+          if constexpr (EPI == EPI_BIAS_RES) {
+            if (v) val += p.res[(size_t)m * p.Cout + col];
+          }
+          if (v) p.out[(size_t)m * p.Cout + col] = val;
+          if constexpr (EPI == EPI_STATS) {
+            const float a1 = v ? val : 0.f;
+            s1[j] += a1;
+            s2[j] += a1 * a1;
+          }
+        }
+      }
+      if constexpr (EPI == EPI_STATS) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          float t1 = s1[j], t2 = s2[j];
+          for (int o = 1; o < p.seg; o <<= 1) {
+            t1 += __shfl_xor(t1, o, 64);
+            t2 += __shfl_xor(t2, o, 64);
+          }
+          t1 += __shfl_xor(t1, 32, 64);
+          t2 += __shfl_xor(t2, 32, 64);
+          const int col = n0 + wn * WN + j * 32 + fr;
+          if (mb < p.M && col < p.Cout && fh == 0 && (fr & (p.seg - 1)) == 0) {
+            const int nn = mb / HW, lg = (mb - nn * HW) / 32;
+            const size_t er = ((size_t)nn * p.nphase + phase) * (HW / 32) + lg;
+            p.rowpart[er * nseg + col / p.seg] = make_float2(t1, t2);
+          }
+        }
+      }
+    }
+    return;
+  }
+  // general case: ConvT phase scatter and / or per-row GroupNorm partials
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     float s1[TN], s2[TN];
@@ -112,21 +190,22 @@ DMX_DEV void igemm_epilogue(const IgemmParams& p, floatx16 (&acc)[BM / 64][BN / 
       const int row = (r & 3) + 8 * (r >> 2) + 4 * fh;
       const int m = m0 + wm * WM + i * 32 + row;
       const bool mv = m < p.M;
-      size_t oidx = 0;
+      size_t oidx = (size_t)m;
       int nn = 0, rr = 0;
-      if (mv) {
+      if (mv && (strided || (EPI == EPI_STATS && p.rgrp != 32))) {
         nn = m / HW;
         rr = m - nn * HW;
-        const int y = rr / p.W, x = rr - y * p.W;
-        const int py = p.geom == 2 ? phase >> 1 : 0, px = p.geom == 2 ? phase & 1 : 0;
-        oidx = ((size_t)nn * p.Hout + (y * p.osy + py)) * p.Wout + (x * p.osx + px);
+        if (strided) {
+          const int y = rr / p.W, x = rr - y * p.W;
+          const int py = phase >> 1, px = phase & 1;
+          oidx = ((size_t)nn * p.Hout + (y * p.osy + py)) * p.Wout + (x * p.osx + px);
+        }
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = n0 + wn * WN + j * 32 + fr;
         const bool v = mv && col < p.Cout;
-        float val = acc[i][j][r];
-        if (p.bias != nullptr && col < p.Cout) val += p.bias[col];
+        float val = acc[i][j][r] + bj[j];
         if constexpr (EPI == EPI_BIAS_GELU) val = gelu(val);
         if constexpr (EPI == EPI_BIAS_RES) {
           if (v) val += p.res[oidx * p.Cout + col];

@@ -88,16 +88,7 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
   for (int i = 0; i < AP; ++i) {
     const int m = m0 + ra + i * ARS;
     rpix[i] = m < p.M ? m : 0;
-    unsigned mk = 0;
-    if (m < p.M) {
-      const int n = m / HW, r = m - n * HW, y = r / p.W, x = r - y * p.W;
-      for (int t = 0; t < p.taps; ++t) {
-        int dy, dx;
-        tap_offset(p.geom, phase, t, dy, dx);
-        if (y + dy >= 0 && y + dy < p.H && x + dx >= 0 && x + dx < p.W) mk |= 1u << t;
-      }
-    }
-    tmask[i] = mk;
+    tmask[i] = tap_mask(p.geom, phase, p.taps, m, p.M, p.H, p.W);
   }
 
   floatx4 ra4[SPLIT_A ? 1 : AP];
@@ -291,16 +282,7 @@ __global__ __launch_bounds__(256) void igemm_x3g_kernel(const X3Params P) {
     achunk[q] = lj ^ ((row >> 2) & 3);
     const int m = m0 + row;
     rpix[q] = m < p.M ? m : 0;
-    unsigned mk = 0;
-    if (m < p.M) {
-      const int n = m / HW, r = m - n * HW, y = r / p.W, x = r - y * p.W;
-      for (int t = 0; t < p.taps; ++t) {
-        int dy, dx;
-        tap_offset(p.geom, phase, t, dy, dx);
-        if (y + dy >= 0 && y + dy < p.H && x + dx >= 0 && x + dx < p.W) mk |= 1u << t;
-      }
-    }
-    tmask[q] = mk;
+    tmask[q] = tap_mask(p.geom, phase, p.taps, m, p.M, p.H, p.W);
   }
   size_t brow[BQ];  // element offset of this lane's B chunk in the [Npad][Kpad] planes (k-tile 0)
 #pragma unroll
