@@ -98,36 +98,73 @@ def cpu_baseline(args):
                       f"(oracle/ref.py, torch-CPU fp32, {threads} threads)"}
 
 
-def roofline(records, pmc=None):
-    """Dominant kernel = the kernel name with the largest summed duration in one eager,
-    event-timed step; achieved = its algorithmic FLOPs / its event-timed duration."""
-    agg = {}
-    for r in records:
-        a = agg.setdefault(r["kernel"], {"ms": 0.0, "flops": 0.0, "bytes": 0.0, "n": 0})
-        a["ms"] += r["ms"]
-        a["flops"] += r["flops"]
-        a["bytes"] += r["bytes"]
-        a["n"] += 1
-    name, a = max(agg.items(), key=lambda kv: kv[1]["ms"])
+MFMA_FAMILIES = ("igemm_x3_kernel", "igemm_x3g_kernel", "igemm_f32_kernel", "attention_x3_kernel",
+                 "attention_kernel", "tok_ln_qkv_kernel", "tok_attn_out_kernel")
+
+
+def family(name):
+    return name.split("<", 1)[0]
+
+
+def _entry(fam, a, pmc_fam):
+    """Roofline entry of one kernel family: algorithmic work per launch / average launch time."""
     avg_ms = a["ms"] / a["n"]
-    flops_per_launch = a["flops"] / a["n"]
-    achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12
-    if name.startswith("igemm_x3"):
-        # fp32 operands as fp16 hi+lo: 3 f16 MFMAs per algorithmic fp32 multiply-add
-        peak, mfma = F16_MFMA_PEAK_TFLOPS / 3.0, "f16 (x3 split: peak = 2500/3 TF of fp32 work)"
+    if fam in MFMA_FAMILIES:
+        per_launch = a["flops"] / a["n"]
+        achieved = per_launch / (avg_ms * 1e-3) / 1e12
+        if "x3" in fam or fam.startswith("tok_"):
+            # fp32 operands as fp16 hi+lo: 3 f16 MFMAs per algorithmic fp32 multiply-add
+            peak, mfma = F16_MFMA_PEAK_TFLOPS / 3.0, "f16 x3 split (peak = 2500/3 TF of fp32 work)"
+        else:
+            peak, mfma = FP32_MFMA_PEAK_TFLOPS, "f32"
+        e = {"kernel": fam, "bound": "mfma", "mfma_dtype": mfma, "achieved": round(achieved, 3),
+             "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+             "flops_per_launch": per_launch}
     else:
-        peak, mfma = FP32_MFMA_PEAK_TFLOPS, "f32"
-    traffic = None
-    if pmc and name in pmc:
-        traffic = pmc[name]
+        per_launch = a["bytes"] / a["n"]
+        achieved = per_launch / (avg_ms * 1e-3) / 1e9
+        e = {"kernel": fam, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "bytes_per_launch": per_launch}
+    e["traffic"] = round(pmc_fam / a["n"]) if pmc_fam is not None else None
+    e["launches"] = a["n"]
+    e["avg_launch_us"] = round(avg_ms * 1e3, 2)
+    return e
+
+
+def roofline(records, pmc=None):
+    """Dominant kernel = the kernel family (name without template arguments: every tile /
+    epilogue instantiation of the implicit-GEMM conv is one kernel) with the largest summed
+    duration in one eager, HIP-event-timed step (events on the launch stream);
+    achieved = its algorithmic FLOPs (MFMA-bound) or bytes (HBM-bound) per launch / its average
+    event-timed launch duration.  `traffic` = PMC HBM bytes per launch (profiles/pmc_traffic.json,
+    averaged over the family's launches in the step) or null."""
+    agg, fams = {}, {}
+    for r in records:
+        for key, d in ((r["kernel"], agg), (family(r["kernel"]), fams)):
+            a = d.setdefault(key, {"ms": 0.0, "flops": 0.0, "bytes": 0.0, "n": 0, "pmc": 0.0, "pmc_ok": True})
+            a["ms"] += r["ms"]
+            a["flops"] += r["flops"]
+            a["bytes"] += r["bytes"]
+            a["n"] += 1
+            if pmc is not None and r["kernel"] in pmc:
+                a["pmc"] += pmc[r["kernel"]]
+            else:
+                a["pmc_ok"] = False
     total_ms = sum(v["ms"] for v in agg.values())
     total_flops = sum(v["flops"] for v in agg.values())
-    return {"kernel": name, "bound": "mfma", "mfma_dtype": mfma, "achieved": round(achieved, 3),
-            "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
-            "launches": a["n"], "avg_launch_us": round(avg_ms * 1e3, 2),
-            "flops_per_launch": flops_per_launch,
-            "step_kernel_ms": round(total_ms, 3),
-            "step_tflops_eager": round(total_flops / (total_ms * 1e-3) / 1e12, 3)}, agg
+    ranked = sorted(fams.items(), key=lambda kv: -kv[1]["ms"])
+    fam, a = ranked[0]
+    rl = _entry(fam, a, a["pmc"] if a["pmc_ok"] else None)
+    rl["share_of_step"] = round(a["ms"] / total_ms, 3)
+    rl["step_kernel_ms"] = round(total_ms, 3)
+    rl["step_tflops_eager"] = round(total_flops / (total_ms * 1e-3) / 1e12, 3)
+    # the next families by time, each against its own roofline
+    rl["others"] = [dict(_entry(f, v, v["pmc"] if v["pmc_ok"] else None), share_of_step=round(v["ms"] / total_ms, 3))
+                    for f, v in ranked[1:5]]
+    for o in rl["others"]:
+        o.pop("flops_per_launch", None)
+        o.pop("bytes_per_launch", None)
+    return rl, agg
 
 
 def main():
