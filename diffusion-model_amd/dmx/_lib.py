@@ -12,7 +12,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdmx.so")
+# DMX_LIB: an alternative in-tree build (same-box A/B of compiler options); default libdmx.so
+LIB_PATH = os.path.join(_HERE, os.environ.get("DMX_LIB", "libdmx.so"))
 
 DMX_UNET_COND_GEOM = 1
 DMX_UNET_COND = 2

@@ -20,14 +20,29 @@ DMX_DEV float silu(float x) { return x / (1.0f + expf(-x)); }
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+
+// fp32 pair -> packed f16 hi pair (v_cvt_pk_f16_f32, RNE) and packed f16 lo pair
+// lo = f16(v - hi): v_fma_mix{lo,hi}_f16 computes v * 1.0 - hi with hi read as f16 and rounds
+// the exact result once to f16 — the same value as f16((float)(v - (float)hi)) (v - hi is
+// exact in fp32 by Sterbenz), in one VOP3P op per element instead of cvt + sub + cvt.
+DMX_DEV void split2u(float a, float b, unsigned& h, unsigned& l) {
+  h = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){a, b}, half2v));
+  unsigned t;
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]" : "=v"(t) : "v"(a), "v"(h));
+  asm("v_fma_mixhi_f16 %0, %1, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(t) : "v"(b), "v"(h));
+  l = t;
+}
+
 // fp32 -> f16 hi + f16 lo (split-precision operand; lo = f16(v - hi) is exact to ~2^-22 |v|)
 DMX_DEV void split4(floatx4 v, half4& h, half4& l) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const _Float16 hi = (_Float16)v[j];
-    h[j] = hi;
-    l[j] = (_Float16)(v[j] - (float)hi);
-  }
+  unsigned h0, h1, l0, l1;
+  split2u(v[0], v[1], h0, l0);
+  split2u(v[2], v[3], h1, l1);
+  h = __builtin_bit_cast(half4, (u32x2){h0, h1});
+  l = __builtin_bit_cast(half4, (u32x2){l0, l1});
 }
 
 // Input-source modes of a convolution / token GEMM (how the A operand's

@@ -35,18 +35,10 @@ struct X3Params {
 };
 
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
-// hi/lo split of two fp32 values as packed f16 pairs: v_cvt_pk_f16_f32 (RNE), two
-// v_cvt_f32_f16, one v_pk_add_f32, v_cvt_pk_f16_f32 — 5 VALU ops per pair.
-DMX_DEV void split2(f32x2 v, unsigned& h, unsigned& l) {
-  const half2v hh = __builtin_convertvector(v, half2v);
-  const half2v ll = __builtin_convertvector(v - __builtin_convertvector(hh, f32x2), half2v);
-  h = __builtin_bit_cast(unsigned, hh);
-  l = __builtin_bit_cast(unsigned, ll);
-}
+// hi/lo split of two fp32 values as packed f16 pairs (common.h split2u: 3 VALU ops per pair).
+DMX_DEV void split2(f32x2 v, unsigned& h, unsigned& l) { split2u(v.x, v.y, h, l); }
 
 template <int BM, int BN, int EPI, int BK = 32, int NBUF = 2, int SPLIT_A = 0>
 __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
