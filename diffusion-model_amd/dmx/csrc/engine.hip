@@ -880,7 +880,12 @@ static void attention_core(Run& R, const float* qkv, float* out, int N, int L, i
   if (R.m->prec == 1) {
     dim3 grid(cdiv(L, 128), 4, N);
     R.begin("attention_x3_kernel<" + std::to_string(D) + ">", 4.0 * N * (double)L * L * C, 4.0 * (double)N * L * 4 * C);
-    if (D == 16) attention_x3_kernel<16><<<grid, 256, 0, R.st>>>(qkv, out, L, C);
+    static const int occ = [] {  // minimum waves per SIMD requested for D = 16 (register cap)
+      const char* e = std::getenv("DMX_ATT_OCC");
+      return e ? std::atoi(e) : 4;
+    }();
+    if (D == 16 && occ >= 4) attention_x3_kernel<16, 4><<<grid, 256, 0, R.st>>>(qkv, out, L, C);
+    else if (D == 16) attention_x3_kernel<16><<<grid, 256, 0, R.st>>>(qkv, out, L, C);
     else if (D == 32) attention_x3_kernel<32><<<grid, 256, 0, R.st>>>(qkv, out, L, C);
     else if (D == 64) attention_x3_kernel<64><<<grid, 256, 0, R.st>>>(qkv, out, L, C);
     else throw Error(DMX_E_INTERNAL, "attention: unsupported head dim");
@@ -921,11 +926,18 @@ static float* attn_block_fused(Run& R, const AttnW& a, const float* x, int N, in
     const std::string cs = std::to_string(C);
     tp.out = qkv;
     tp.w0 = tokw(a.qkv);
-    const int nb = C == 64 ? 64 : 128;  // output columns per block (grid.y = 3C / nb)
+    static const int nb64 = [] {  // C = 64: all 3C = 192 columns per block (LN1 + x read once)
+      const char* e = std::getenv("DMX_TOK_NB64");
+      return e ? std::atoi(e) : 192;
+    }();
+    const int nb = C == 64 ? nb64 : 128;  // output columns per block (grid.y = 3C / nb)
     const dim3 grid(cdiv(M, 64), 3 * C / nb);
     R.begin("tok_ln_qkv_kernel<" + cs + ", " + std::to_string(nb) + ">", 2.0 * M * C * 3.0 * C, 16.0 * (double)M * C);
     switch (C) {
-      case 64: tok_ln_qkv_kernel<64, 64><<<grid, 256, 0, R.st>>>(tp); break;
+      case 64:
+        if (nb == 192) tok_ln_qkv_kernel<64, 192><<<grid, 256, 0, R.st>>>(tp);
+        else tok_ln_qkv_kernel<64, 64><<<grid, 256, 0, R.st>>>(tp);
+        break;
       case 128: tok_ln_qkv_kernel<128, 128><<<grid, 256, 0, R.st>>>(tp); break;
       default: tok_ln_qkv_kernel<256, 128><<<grid, 256, 0, R.st>>>(tp); break;
     }

@@ -429,8 +429,9 @@ namespace dmx {
 // of k-step s (row 16s + 8(j>>2) + 4h + (j&3) of the tile), and V^T is read with the same
 // key permutation.  D = 16 pads V^T to 32 rows (zero).
 // ---------------------------------------------------------------------------
-template <int D>
-__global__ __launch_bounds__(256) void attention_x3_kernel(const float* qkv, float* out, int L, int C) {
+template <int D, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void attention_x3_kernel(
+    const float* qkv, float* out, int L, int C) {
   constexpr int KC = 64, KS = D + 8, VR = D < 32 ? 32 : D, VS = KC + 4, NKS = D / 16, NDT = VR / 32;
   __shared__ __attribute__((aligned(16))) _Float16 Kh[KC][KS];
   __shared__ __attribute__((aligned(16))) _Float16 Kl[KC][KS];
