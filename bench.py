@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=3, help="oracle steps timed for cpu_baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--config4-steps", type=int, default=100,
+                    help="steps timed in BASELINE config 4 (fp16 arithmetic) beside the headline (0 = skip)")
     return ap.parse_args()
 
 
@@ -167,6 +169,30 @@ def roofline(records, pmc=None):
     return rl, agg
 
 
+def config4(nm, x, y, vals, mask, args, tables, seed):
+    """BASELINE config 4: the same CFG step with fp16 GEMM/attention operands (one f16 MFMA,
+    fp32 accumulate, fp32 norms/softmax/scheduler); tolerance study in tests/test_gpu_f16.py.
+    Reported beside the headline, never as `value` (reduced precision)."""
+    nm.set_precision("f16")
+    try:
+        xs = x.clone()
+        t_dev = torch.full((1,), args.T, dtype=torch.long, device=x.device)
+        nm.sample_loop(xs, t_dev, y, 0, vals, mask, args.guidance, tables, 5, seed=seed)  # warm-up + capture
+        torch.cuda.synchronize()
+        t_dev.fill_(args.T)
+        t0 = time.perf_counter()
+        nm.sample_loop(xs, t_dev, y, 0, vals, mask, args.guidance, tables, args.config4_steps, seed=seed)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        assert torch.isfinite(xs).all(), "non-finite latents (config 4)"
+    finally:
+        nm.set_precision("x3")
+    return {"workload": "config 4: config 2 with fp16 weights/activations, fp32 accumulate + scheduler",
+            "value": round(args.config4_steps / dt, 3), "unit": "CFG batch-steps/s (B=%d)" % args.batch,
+            "ms_per_step": round(dt / args.config4_steps * 1e3, 4), "steps": args.config4_steps, "dtype": "f16",
+            "tolerance": "latents rel-L2 <= 2e-3 after T=1000, measured 7.1e-4 (tests/test_gpu_f16.py)"}
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
@@ -233,6 +259,8 @@ def main():
         "sample_steps_per_s": round(value * args.batch, 1),
         "tflops_effective": round(value * 2 * args.batch * UNET_GFLOP_PER_SAMPLE / 1e3, 2),
     }
+    if world == 1 and args.config4_steps > 0:
+        out["config4"] = config4(nm, x, y, vals, mask, args, tables, seed)
     if rank == 0:
         if not args.no_profile:
             xp = x.clone()

@@ -243,7 +243,7 @@ struct dmx_model {
   bool has_graph = false;
   // debug taps: (name, device pointer into the workspace, element count, C)
   bool debug = false;
-  int prec = 1;  // 0: fp32 MFMA (exact fp32 products), 1: fp16 hi/lo x3 split MFMA
+  int prec = 1;  // 0: fp32 MFMA (exact fp32 products), 1: fp16 hi/lo x3 split MFMA, 2: fp16 (config 4)
   std::vector<std::pair<std::string, std::pair<const float*, size_t>>> taps;
 };
 
@@ -569,18 +569,18 @@ static bool split_a_enabled() {
   return v;
 }
 
-template <int EPI, int BK, int NB, int SA>
+template <int EPI, int BK, int NB, int SA, int X1 = 0>
 static void launch_x3_s(int bm, int bn, const X3Params& p, dim3 grid, hipStream_t st) {
-  if (bm == 128 && bn == 128) igemm_x3_kernel<128, 128, EPI, BK, NB, SA><<<grid, 256, 0, st>>>(p);
-  else if (bm == 128) igemm_x3_kernel<128, 64, EPI, BK, NB, SA><<<grid, 256, 0, st>>>(p);
-  else if (bn == 128) igemm_x3_kernel<64, 128, EPI, BK, NB, SA><<<grid, 256, 0, st>>>(p);
-  else igemm_x3_kernel<64, 64, EPI, BK, NB, SA><<<grid, 256, 0, st>>>(p);
+  if (bm == 128 && bn == 128) igemm_x3_kernel<128, 128, EPI, BK, NB, SA, X1><<<grid, 256, 0, st>>>(p);
+  else if (bm == 128) igemm_x3_kernel<128, 64, EPI, BK, NB, SA, X1><<<grid, 256, 0, st>>>(p);
+  else if (bn == 128) igemm_x3_kernel<64, 128, EPI, BK, NB, SA, X1><<<grid, 256, 0, st>>>(p);
+  else igemm_x3_kernel<64, 64, EPI, BK, NB, SA, X1><<<grid, 256, 0, st>>>(p);
 }
 
-template <int EPI, int BK, int NB>
+template <int EPI, int BK, int NB, int X1 = 0>
 static void launch_x3_v(int bm, int bn, const X3Params& p, dim3 grid, hipStream_t st) {
-  if (p.Ash != nullptr) launch_x3_s<EPI, BK, NB, 1>(bm, bn, p, grid, st);
-  else launch_x3_s<EPI, BK, NB, 0>(bm, bn, p, grid, st);
+  if (p.Ash != nullptr) launch_x3_s<EPI, BK, NB, 1, X1>(bm, bn, p, grid, st);
+  else launch_x3_s<EPI, BK, NB, 0, X1>(bm, bn, p, grid, st);
 }
 
 // LDS-DMA pipeline for split-plane A operands, opt-in (DMX_GLDS=1; DMX_GLDS_ST=2|3 stages).
@@ -617,7 +617,11 @@ static void launch_x3g(int bm, int bn, const X3Params& p, dim3 grid, hipStream_t
 }
 
 template <int EPI>
-static void launch_x3_tiles(int bm, int bn, const X3Params& p, dim3 grid, hipStream_t st) {
+static void launch_x3_tiles(int bm, int bn, const X3Params& p, dim3 grid, hipStream_t st, bool x1) {
+  if (x1) {  // config-4 fp16 arithmetic: BK 64, register-staged pipeline only
+    launch_x3_v<EPI, 64, 1, 1>(bm, bn, p, grid, st);
+    return;
+  }
   if (p.Ash != nullptr && glds_enabled() && p.g.src.C % 8 == 0) {
     launch_x3g<EPI>(bm, bn, p, grid, st);
     return;
@@ -642,9 +646,10 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   const int tiles128 = cdiv(M, 128) * cdiv(cw.cout, bn) * cw.phases;
   const int bm = tiles128 >= 512 ? 128 : 64;
   const int blocks = cdiv(M, bm) * cdiv(cw.cout, bn) * cw.phases;
-  const bool x3 = R.m->prec == 1 && src_mode == SRC_PLAIN && cw.Bh != nullptr;
-  const bool x3g = x3 && ash != nullptr && glds_enabled() && s.C % 8 == 0;  // LDS-DMA kernel (BK 32)
-  const int bk = x3g ? 32 : x3 ? (x3_pipe() == 2 ? 64 : X3_BK) : IG_BK;
+  const bool x3 = R.m->prec >= 1 && src_mode == SRC_PLAIN && cw.Bh != nullptr;
+  const bool x1 = x3 && R.m->prec == 2;  // config-4 fp16: one MFMA on the hi planes
+  const bool x3g = x3 && !x1 && ash != nullptr && glds_enabled() && s.C % 8 == 0;  // LDS-DMA kernel (BK 32)
+  const int bk = x3g ? 32 : x1 ? 64 : x3 ? (x3_pipe() == 2 ? 64 : X3_BK) : IG_BK;
   const int nkt = cw.kpad / bk;
   int splits = 1, ksplit = nkt;
   static const int split_below = [] {  // split K when the grid has fewer blocks than this
@@ -697,7 +702,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   xp.inv_scale = cw.inv_scale;
   // labels are the demangled kernel names rocprofv3 reports (profiles/ cross-check)
   const char* kname = x3 ? "igemm_x3_kernel" : "igemm_f32_kernel";
-  const int x3_nbuf = (x3_pipe() == 1 || x3_pipe() == 2) ? 1 : 2, x3_sa = ash != nullptr ? 1 : 0;
+  const int x3_nbuf = (x1 || x3_pipe() == 1 || x3_pipe() == 2) ? 1 : 2, x3_sa = ash != nullptr ? 1 : 0;
   const int creal = (src_mode == SRC_NCHW && s.C0) ? s.C0 : cw.cin;
   const double flops = 2.0 * (double)M * cw.phases * cw.cout * (double)cw.taps * creal;
   const double bytes = 4.0 * ((double)M * cw.phases * cw.cout + (double)M * s.C +
@@ -706,11 +711,11 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   if (splits > 1) {
     dim3 grid(cdiv(M, bm), cdiv(cw.cout, bn), splits);
     if (x3g) std::snprintf(nm, sizeof nm, "igemm_x3g_kernel<%d, %d, %d, %d>", bm, bn, (int)EPI_PARTIAL, glds_stages() == 2 ? 2 : 3);
-    else if (x3) std::snprintf(nm, sizeof nm, "%s<%d, %d, %d, %d, %d, %d>", kname, bm, bn, (int)EPI_PARTIAL, bk, x3_nbuf,
-                               x3_sa);
+    else if (x3) std::snprintf(nm, sizeof nm, "%s<%d, %d, %d, %d, %d, %d, %d>", kname, bm, bn, (int)EPI_PARTIAL, bk,
+                               x3_nbuf, x3_sa, x1 ? 1 : 0);
     else std::snprintf(nm, sizeof nm, "%s<%d, %d, %d, %d>", kname, bm, bn, src_mode, (int)EPI_PARTIAL);
     R.begin(nm, flops, bytes + 4.0 * splits * M * cw.cout);
-    if (x3) launch_x3_tiles<EPI_PARTIAL>(bm, bn, xp, grid, R.st);
+    if (x3) launch_x3_tiles<EPI_PARTIAL>(bm, bn, xp, grid, R.st, x1);
     else if (src_mode == SRC_NCHW) launch_ig_tiles<SRC_NCHW, EPI_PARTIAL>(bm, bn, p, grid, R.st);
     else launch_ig_tiles<SRC_PLAIN, EPI_PARTIAL>(bm, bn, p, grid, R.st);
     R.end();
@@ -725,15 +730,16 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   }
   dim3 grid(cdiv(M, bm), cdiv(cw.cout, bn), cw.phases);
   if (x3g) std::snprintf(nm, sizeof nm, "igemm_x3g_kernel<%d, %d, %d, %d>", bm, bn, epi, glds_stages() == 2 ? 2 : 3);
-  else if (x3) std::snprintf(nm, sizeof nm, "%s<%d, %d, %d, %d, %d, %d>", kname, bm, bn, epi, bk, x3_nbuf, x3_sa);
+  else if (x3) std::snprintf(nm, sizeof nm, "%s<%d, %d, %d, %d, %d, %d, %d>", kname, bm, bn, epi, bk, x3_nbuf, x3_sa,
+                             x1 ? 1 : 0);
   else std::snprintf(nm, sizeof nm, "%s<%d, %d, %d, %d>", kname, bm, bn, epi == EPI_STATS ? src_mode : SRC_PLAIN, epi);
   R.begin(nm, flops, bytes);
   if (x3) {
     switch (epi) {
-      case EPI_STATS: launch_x3_tiles<EPI_STATS>(bm, bn, xp, grid, R.st); break;
-      case EPI_BIAS: launch_x3_tiles<EPI_BIAS>(bm, bn, xp, grid, R.st); break;
-      case EPI_BIAS_GELU: launch_x3_tiles<EPI_BIAS_GELU>(bm, bn, xp, grid, R.st); break;
-      case EPI_BIAS_RES: launch_x3_tiles<EPI_BIAS_RES>(bm, bn, xp, grid, R.st); break;
+      case EPI_STATS: launch_x3_tiles<EPI_STATS>(bm, bn, xp, grid, R.st, x1); break;
+      case EPI_BIAS: launch_x3_tiles<EPI_BIAS>(bm, bn, xp, grid, R.st, x1); break;
+      case EPI_BIAS_GELU: launch_x3_tiles<EPI_BIAS_GELU>(bm, bn, xp, grid, R.st, x1); break;
+      case EPI_BIAS_RES: launch_x3_tiles<EPI_BIAS_RES>(bm, bn, xp, grid, R.st, x1); break;
       default: throw Error(DMX_E_INTERNAL, "bad epilogue");
     }
     R.end();
@@ -827,7 +833,7 @@ static float* resblock(Run& R, const ResW& w, const SrcDesc& in, int mode, int N
   const int seg = 32;
   float* r1 = R.ws.get<float>((size_t)M * w.mid);
   float2* rp1 = R.ws.get<float2>((size_t)M * (w.mid / seg));
-  const bool planes = R.m->prec == 1 && split_a_enabled() && w.c2.Bh != nullptr && w.mid >= 64;
+  const bool planes = R.m->prec >= 1 && split_a_enabled() && w.c2.Bh != nullptr && w.mid >= 64;
   float* a1 = R.ws.get<float>((size_t)M * w.mid);  // fp32 or, with planes, hi|lo f16 halves
   float* r2 = R.ws.get<float>((size_t)M * w.cout);
   float2* rp2 = R.ws.get<float2>((size_t)M * (w.cout / seg));
@@ -877,18 +883,21 @@ static void layernorm(Run& R, const float* x, float* y, const Vec& w, const Vec&
 static void attention_core(Run& R, const float* qkv, float* out, int N, int L, int C) {
   if (R.plan) return;
   const int D = C / 4;
-  if (R.m->prec == 1) {
+  if (R.m->prec >= 1) {
     dim3 grid(cdiv(L, 128), 4, N);
-    R.begin("attention_x3_kernel<" + std::to_string(D) + ">", 4.0 * N * (double)L * L * C, 4.0 * (double)N * L * 4 * C);
     static const int occ = [] {  // minimum waves per SIMD requested for D = 16 (register cap)
       const char* e = std::getenv("DMX_ATT_OCC");
       return e ? std::atoi(e) : 4;
     }();
-    if (D == 16 && occ >= 4) attention_x3_kernel<16, 4><<<grid, 256, 0, R.st>>>(qkv, out, L, C);
-    else if (D == 16) attention_x3_kernel<16><<<grid, 256, 0, R.st>>>(qkv, out, L, C);
-    else if (D == 32) attention_x3_kernel<32><<<grid, 256, 0, R.st>>>(qkv, out, L, C);
-    else if (D == 64) attention_x3_kernel<64><<<grid, 256, 0, R.st>>>(qkv, out, L, C);
+    const int x1 = R.m->prec == 2 ? 1 : 0, wpe = (D == 16 && occ >= 4) ? 4 : 1;
+    R.begin("attention_x3_kernel<" + std::to_string(D) + ", " + std::to_string(wpe) + ", " + std::to_string(x1) + ">",
+            4.0 * N * (double)L * L * C, 4.0 * (double)N * L * 4 * C);
+#define ATX(DD, W, X) attention_x3_kernel<DD, W, X><<<grid, 256, 0, R.st>>>(qkv, out, L, C)
+    if (D == 16) { if (wpe == 4) { if (x1) ATX(16, 4, 1); else ATX(16, 4, 0); } else { if (x1) ATX(16, 1, 1); else ATX(16, 1, 0); } }
+    else if (D == 32) { if (x1) ATX(32, 1, 1); else ATX(32, 1, 0); }
+    else if (D == 64) { if (x1) ATX(64, 1, 1); else ATX(64, 1, 0); }
     else throw Error(DMX_E_INTERNAL, "attention: unsupported head dim");
+#undef ATX
     R.end();
     HIPCHK(hipGetLastError());
     return;
@@ -932,15 +941,20 @@ static float* attn_block_fused(Run& R, const AttnW& a, const float* x, int N, in
     }();
     const int nb = C == 64 ? nb64 : 128;  // output columns per block (grid.y = 3C / nb)
     const dim3 grid(cdiv(M, 64), 3 * C / nb);
-    R.begin("tok_ln_qkv_kernel<" + cs + ", " + std::to_string(nb) + ">", 2.0 * M * C * 3.0 * C, 16.0 * (double)M * C);
+    const int x1 = R.m->prec == 2 ? 1 : 0;
+    R.begin("tok_ln_qkv_kernel<" + cs + ", " + std::to_string(nb) + ", " + std::to_string(x1) + ">",
+            2.0 * M * C * 3.0 * C, 16.0 * (double)M * C);
+#define TQ(CC, NN) (x1 ? tok_ln_qkv_kernel<CC, NN, 1><<<grid, 256, 0, R.st>>>(tp) \
+                       : tok_ln_qkv_kernel<CC, NN, 0><<<grid, 256, 0, R.st>>>(tp))
     switch (C) {
       case 64:
-        if (nb == 192) tok_ln_qkv_kernel<64, 192><<<grid, 256, 0, R.st>>>(tp);
-        else tok_ln_qkv_kernel<64, 64><<<grid, 256, 0, R.st>>>(tp);
+        if (nb == 192) TQ(64, 192);
+        else TQ(64, 64);
         break;
-      case 128: tok_ln_qkv_kernel<128, 128><<<grid, 256, 0, R.st>>>(tp); break;
-      default: tok_ln_qkv_kernel<256, 128><<<grid, 256, 0, R.st>>>(tp); break;
+      case 128: TQ(128, 128); break;
+      default: TQ(256, 128); break;
     }
+#undef TQ
     R.end();
     HIPCHK(hipGetLastError());
   }
@@ -961,12 +975,17 @@ static float* attn_block_fused(Run& R, const AttnW& a, const float* x, int N, in
     // 32-token tiles when 64-token tiles would leave the chip under-filled (or C = 256)
     const int tm = C == 64 ? 64 : (C == 256 || cdiv(M, 64) < 512) ? 32 : 64;
     const int blocks = cdiv(M, tm);
-    R.begin("tok_attn_out_kernel<" + std::to_string(C) + ", " + std::to_string(tm) + ">", 6.0 * M * (double)C * C,
+    const int x1 = R.m->prec == 2 ? 1 : 0;
+    R.begin("tok_attn_out_kernel<" + std::to_string(C) + ", " + std::to_string(tm) + ", " + std::to_string(x1) + ">",
+            6.0 * M * (double)C * C,
             12.0 * (double)M * C);
-    if (C == 64) tok_attn_out_kernel<64, 64><<<blocks, 256, 0, R.st>>>(tp);
-    else if (C == 128 && tm == 64) tok_attn_out_kernel<128, 64><<<blocks, 256, 0, R.st>>>(tp);
-    else if (C == 128) tok_attn_out_kernel<128, 32><<<blocks, 256, 0, R.st>>>(tp);
-    else tok_attn_out_kernel<256, 32><<<blocks, 256, 0, R.st>>>(tp);
+#define TB(CC, TT) (x1 ? tok_attn_out_kernel<CC, TT, 1><<<blocks, 256, 0, R.st>>>(tp) \
+                       : tok_attn_out_kernel<CC, TT, 0><<<blocks, 256, 0, R.st>>>(tp))
+    if (C == 64) TB(64, 64);
+    else if (C == 128 && tm == 64) TB(128, 64);
+    else if (C == 128) TB(128, 32);
+    else TB(256, 32);
+#undef TB
     R.end();
     HIPCHK(hipGetLastError());
   }
@@ -987,7 +1006,7 @@ static bool tok_fused_enabled() {
 // AttenionBlock (models/unet_cond.py:32-52) on NHWC == (N, L, C) tokens.
 static float* attn_block(Run& R, const AttnW& a, const float* x, int N, int H, int W) {
   const int C = a.c, M = N * H * W, L = H * W;
-  if (R.m->prec == 1 && tok_fused_enabled() && (C == 64 || C == 128 || C == 256) && a.qkv.kpad == C &&
+  if (R.m->prec >= 1 && tok_fused_enabled() && (C == 64 || C == 128 || C == 256) && a.qkv.kpad == C &&
       a.o.kpad == C && a.f1.kpad == C && a.f2.kpad == C)
     return attn_block_fused(R, a, x, N, H, W);
   float* xl = R.ws.get<float>((size_t)M * C);
@@ -1394,7 +1413,7 @@ int64_t dmx_model_workspace_bytes(const dmx_model* m) { return m ? (int64_t)m->w
 int dmx_model_set_precision(dmx_model* m, int prec) {
   return guarded([&] {
     REQUIRE(m != nullptr, "null model");
-    REQUIRE(prec == 0 || prec == 1, "precision must be 0 (fp32 MFMA) or 1 (fp16x3 split)");
+    REQUIRE(prec >= 0 && prec <= 2, "precision must be 0 (fp32 MFMA), 1 (fp16x3 split) or 2 (fp16, config 4)");
     if (m->prec != prec && m->has_graph) {
       (void)hipGraphExecDestroy(m->gexec);
       (void)hipGraphDestroy(m->graph);

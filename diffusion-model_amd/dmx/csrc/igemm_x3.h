@@ -40,7 +40,9 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 // hi/lo split of two fp32 values as packed f16 pairs (common.h split2u: 3 VALU ops per pair).
 DMX_DEV void split2(f32x2 v, unsigned& h, unsigned& l) { split2u(v.x, v.y, h, l); }
 
-template <int BM, int BN, int EPI, int BK = 32, int NBUF = 2, int SPLIT_A = 0>
+// X1 = 1: config-4 fp16 arithmetic — operands rounded to f16 (hi planes only), ONE MFMA per
+// product (ah*bh), fp32 accumulate; the lo planes are neither loaded nor stored.
+template <int BM, int BN, int EPI, int BK = 32, int NBUF = 2, int SPLIT_A = 0, int X1 = 0>
 __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
   const IgemmParams& p = P.g;
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
@@ -52,10 +54,11 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
   constexpr int ARS = 256 / APR, BRS = 256 / BPR;  // rows covered per pass
   static_assert(TM >= 1 && TN >= 1 && AP >= 1 && BP >= 1, "tile");
 
+  constexpr int LA = X1 ? 1 : BM, LB = X1 ? 1 : BN;  // lo planes (unused with X1)
   __shared__ __attribute__((aligned(16))) _Float16 Ah[NBUF][BM][RS];
-  __shared__ __attribute__((aligned(16))) _Float16 Al[NBUF][BM][RS];
+  __shared__ __attribute__((aligned(16))) _Float16 Al[NBUF][LA][RS];
   __shared__ __attribute__((aligned(16))) _Float16 Bhs[NBUF][BN][RS];
-  __shared__ __attribute__((aligned(16))) _Float16 Bls[NBUF][BN][RS];
+  __shared__ __attribute__((aligned(16))) _Float16 Bls[NBUF][LB][RS];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
@@ -113,9 +116,11 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
       const int off = (rpix[i] + delta) * C + c;
       if constexpr (SPLIT_A) {
         const _Float16* ph = ok ? P.Ash + off : reinterpret_cast<const _Float16*>(g_zero16);
-        const _Float16* pl = ok ? P.Asl + off : reinterpret_cast<const _Float16*>(g_zero16);
         rah[i] = *reinterpret_cast<const half8*>(ph);
-        ral[i] = *reinterpret_cast<const half8*>(pl);
+        if constexpr (!X1) {
+          const _Float16* pl = ok ? P.Asl + off : reinterpret_cast<const _Float16*>(g_zero16);
+          ral[i] = *reinterpret_cast<const half8*>(pl);
+        }
       } else {
         ra4[i] = ld4(ok ? asrc + off : g_zero16);
       }
@@ -124,7 +129,7 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
     for (int i = 0; i < BP; ++i) {
       const size_t o = (size_t)(n0 + rb + i * BRS) * p.Kpad + kt * BK + qb * 8;
       rbh[i] = *reinterpret_cast<const half8*>(Bh + o);
-      rbl[i] = *reinterpret_cast<const half8*>(Bl + o);
+      if constexpr (!X1) rbl[i] = *reinterpret_cast<const half8*>(Bl + o);
     }
   };
   auto store_tile = [&](int buf) {
@@ -132,7 +137,9 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
     for (int i = 0; i < AP; ++i) {
       if constexpr (SPLIT_A) {
         *reinterpret_cast<half8*>(&Ah[buf][ra + i * ARS][qa * 8]) = rah[i];
-        *reinterpret_cast<half8*>(&Al[buf][ra + i * ARS][qa * 8]) = ral[i];
+        if constexpr (!X1) *reinterpret_cast<half8*>(&Al[buf][ra + i * ARS][qa * 8]) = ral[i];
+      } else if constexpr (X1) {
+        *reinterpret_cast<half4*>(&Ah[buf][ra + i * ARS][qa * 4]) = __builtin_convertvector(ra4[i], half4);
       } else {
         half4 h, l;
         split4(ra4[i], h, l);
@@ -143,7 +150,7 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
 #pragma unroll
     for (int i = 0; i < BP; ++i) {
       *reinterpret_cast<half8*>(&Bhs[buf][rb + i * BRS][qb * 8]) = rbh[i];
-      *reinterpret_cast<half8*>(&Bls[buf][rb + i * BRS][qb * 8]) = rbl[i];
+      if constexpr (!X1) *reinterpret_cast<half8*>(&Bls[buf][rb + i * BRS][qb * 8]) = rbl[i];
     }
   };
 
@@ -164,20 +171,22 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
       for (int i = 0; i < TM; ++i) {
         const int row = wm * WM + i * 32 + fr;
         ah[i] = *reinterpret_cast<const half8*>(&Ah[buf][row][16 * s + 8 * fh]);
-        al[i] = *reinterpret_cast<const half8*>(&Al[buf][row][16 * s + 8 * fh]);
+        if constexpr (!X1) al[i] = *reinterpret_cast<const half8*>(&Al[buf][row][16 * s + 8 * fh]);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * WN + j * 32 + fr;
         bh[j] = *reinterpret_cast<const half8*>(&Bhs[buf][row][16 * s + 8 * fh]);
-        bl[j] = *reinterpret_cast<const half8*>(&Bls[buf][row][16 * s + 8 * fh]);
+        if constexpr (!X1) bl[j] = *reinterpret_cast<const half8*>(&Bls[buf][row][16 * s + 8 * fh]);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          if constexpr (!X1) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          }
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
         }
     }
@@ -429,14 +438,15 @@ namespace dmx {
 // of k-step s (row 16s + 8(j>>2) + 4h + (j&3) of the tile), and V^T is read with the same
 // key permutation.  D = 16 pads V^T to 32 rows (zero).
 // ---------------------------------------------------------------------------
-template <int D, int WPE = 1>
+// X1 = 1: config-4 fp16 arithmetic (Q, K, V, P rounded to f16, one MFMA per product).
+template <int D, int WPE = 1, int X1 = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void attention_x3_kernel(
     const float* qkv, float* out, int L, int C) {
   constexpr int KC = 64, KS = D + 8, VR = D < 32 ? 32 : D, VS = KC + 4, NKS = D / 16, NDT = VR / 32;
   __shared__ __attribute__((aligned(16))) _Float16 Kh[KC][KS];
-  __shared__ __attribute__((aligned(16))) _Float16 Kl[KC][KS];
+  __shared__ __attribute__((aligned(16))) _Float16 Kl[X1 ? 1 : KC][KS];
   __shared__ __attribute__((aligned(16))) _Float16 Vh[VR][VS];
-  __shared__ __attribute__((aligned(16))) _Float16 Vl[VR][VS];
+  __shared__ __attribute__((aligned(16))) _Float16 Vl[X1 ? 1 : VR][VS];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int hd = blockIdx.y, n = blockIdx.z;
   const int fr = lane & 31, fh = lane >> 5;
@@ -472,7 +482,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     for (int i = tid; i < (VR - D) * VS; i += 256) {
       const int r = D + i / VS;
       Vh[r][i % VS] = (_Float16)(r == D ? 1.f : 0.f);
-      Vl[r][i % VS] = (_Float16)0.f;
+      if constexpr (!X1) Vl[r][i % VS] = (_Float16)0.f;
     }
   }
   floatx16 o[NDT];
@@ -505,6 +515,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       const bool kvalid = c0 + key < L;  // keys past L: zero K / V (their scores are masked)
       const floatx4 z = {0.f, 0.f, 0.f, 0.f};
       half4 h, l;
+      if constexpr (X1) {
+        *reinterpret_cast<half4*>(&Kh[key][d4]) = __builtin_convertvector(kvalid ? kr[it] : z, half4);
+        h = __builtin_convertvector(kvalid ? vr[it] : z, half4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) Vh[d4 + j][key] = h[j];
+        continue;
+      }
       split4(kvalid ? kr[it] : z, h, l);
       *reinterpret_cast<half4*>(&Kh[key][d4]) = h;
       *reinterpret_cast<half4*>(&Kl[key][d4]) = l;
@@ -526,9 +543,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
         const half8 kh = *reinterpret_cast<const half8*>(&Kh[kt * 32 + fr][16 * ks + 8 * fh]);
-        const half8 kl = *reinterpret_cast<const half8*>(&Kl[kt * 32 + fr][16 * ks + 8 * fh]);
-        sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kl, qh[ks], sc[kt], 0, 0, 0);
-        sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, ql[ks], sc[kt], 0, 0, 0);
+        if constexpr (!X1) {
+          const half8 kl = *reinterpret_cast<const half8*>(&Kl[kt * 32 + fr][16 * ks + 8 * fh]);
+          sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kl, qh[ks], sc[kt], 0, 0, 0);
+          sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, ql[ks], sc[kt], 0, 0, 0);
+        }
         sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, qh[ks], sc[kt], 0, 0, 0);
       }
     }
@@ -567,7 +586,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           v.y = __builtin_amdgcn_exp2f(v.y);
           if constexpr (!ONES) ls2 += v;
           unsigned h, l;
-          split2(v, h, l);
+          if constexpr (X1) {
+            h = __builtin_bit_cast(unsigned, __builtin_convertvector(v, half2v));
+            l = 0u;
+          } else {
+            split2(v, h, l);
+          }
           phu[kt][s][jp] = h;
           plu[kt][s][jp] = l;
         }
@@ -595,17 +619,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           half8 vh, vl;
           const half4 a0 = *reinterpret_cast<const half4*>(&Vh[d][k0]);
           const half4 a1 = *reinterpret_cast<const half4*>(&Vh[d][k0 + 8]);
-          const half4 b0 = *reinterpret_cast<const half4*>(&Vl[d][k0]);
-          const half4 b1 = *reinterpret_cast<const half4*>(&Vl[d][k0 + 8]);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             vh[j] = a0[j];
             vh[j + 4] = a1[j];
-            vl[j] = b0[j];
-            vl[j + 4] = b1[j];
           }
-          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph, o[dt], 0, 0, 0);
-          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, pl, o[dt], 0, 0, 0);
+          if constexpr (!X1) {
+            const half4 b0 = *reinterpret_cast<const half4*>(&Vl[d][k0]);
+            const half4 b1 = *reinterpret_cast<const half4*>(&Vl[d][k0 + 8]);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              vl[j] = b0[j];
+              vl[j + 4] = b1[j];
+            }
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph, o[dt], 0, 0, 0);
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, pl, o[dt], 0, 0, 0);
+          }
           o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, o[dt], 0, 0, 0);
         }
       }

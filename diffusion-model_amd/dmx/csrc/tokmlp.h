@@ -136,7 +136,7 @@ DMX_DEV void tok_rows(const float* src, int ld, int m0, int M, const float* g, c
 // acc[j] = A[arow0 .. +32][0, C) . W[nw + 32j .. +32][0, C)^T  (x3 sum, still scaled by 2^e).
 // B fragments come straight from global memory (L2-resident weights) with a PD-step
 // rolling register prefetch.
-template <int C, int NT>
+template <int C, int NT, int X1 = 0>
 DMX_DEV void tok_gemm(const _Float16 (*Ah)[C + 8], const _Float16 (*Al)[C + 8], const TokW& w, int nw,
                       floatx16 (&acc)[NT], int arow0, int fr, int fh) {
   constexpr int S = C / 16, PD = S < 4 ? S : 4;
@@ -152,7 +152,7 @@ DMX_DEV void tok_gemm(const _Float16 (*Ah)[C + 8], const _Float16 (*Al)[C + 8], 
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       h[j] = *reinterpret_cast<const half8*>(wh + j * jstride + 16 * s);
-      l[j] = *reinterpret_cast<const half8*>(wl + j * jstride + 16 * s);
+      if constexpr (!X1) l[j] = *reinterpret_cast<const half8*>(wl + j * jstride + 16 * s);
     }
   };
 #pragma unroll
@@ -161,7 +161,8 @@ DMX_DEV void tok_gemm(const _Float16 (*Ah)[C + 8], const _Float16 (*Al)[C + 8], 
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const half8 ah = *reinterpret_cast<const half8*>(&Ah[arow][16 * s + 8 * fh]);
-    const half8 al = *reinterpret_cast<const half8*>(&Al[arow][16 * s + 8 * fh]);
+    half8 al;
+    if constexpr (!X1) al = *reinterpret_cast<const half8*>(&Al[arow][16 * s + 8 * fh]);
     half8 ch[NT], cl[NT];
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
@@ -171,8 +172,10 @@ DMX_DEV void tok_gemm(const _Float16 (*Ah)[C + 8], const _Float16 (*Al)[C + 8], 
     if (s + PD < S) loadb(s + PD, bh[s % PD], bl[s % PD]);
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, ch[j], acc[j], 0, 0, 0);
-      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, cl[j], acc[j], 0, 0, 0);
+      if constexpr (!X1) {
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, ch[j], acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, cl[j], acc[j], 0, 0, 0);
+      }
       acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ch[j], acc[j], 0, 0, 0);
     }
   }
@@ -183,7 +186,7 @@ DMX_DEV int tok_r(int fh, int r) { return (r & 3) + 8 * (r >> 2) + 4 * fh; }
 
 // TA: qkv = LN1(x) Wqkv^T + b_in (nn.MultiheadAttention in_proj on the LN1 output).
 // Block = 64 tokens x NB of the 3C output columns (grid.y = 3C / NB); waves 2 x 2.
-template <int C, int NB>
+template <int C, int NB, int X1 = 0>
 __global__ __launch_bounds__(256) void tok_ln_qkv_kernel(const TokParams P) {
   constexpr int NT = NB / 64;
   __shared__ __attribute__((aligned(16))) _Float16 Ah[64][C + 8];
@@ -194,7 +197,7 @@ __global__ __launch_bounds__(256) void tok_ln_qkv_kernel(const TokParams P) {
   __syncthreads();
   const int nw = blockIdx.y * NB + wn * (NB / 2);
   floatx16 acc[NT];
-  tok_gemm<C, NT>(Ah, Al, P.w0, nw, acc, wm * 32, fr, fh);
+  tok_gemm<C, NT, X1>(Ah, Al, P.w0, nw, acc, wm * 32, fr, fh);
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     const int col = nw + 32 * j + fr;
@@ -209,7 +212,7 @@ __global__ __launch_bounds__(256) void tok_ln_qkv_kernel(const TokParams P) {
 
 // TB: out-proj + residual, LN2, FF1 + GELU, FF2 + residual for TM tokens x all C channels.
 // TM = 64: waves 2 (rows) x 2 (cols); TM = 32: 1 x 4 (more blocks for small M / wide C).
-template <int C, int TM>
+template <int C, int TM, int X1 = 0>
 __global__ __launch_bounds__(256) void tok_attn_out_kernel(const TokParams P) {
   constexpr int WR = TM / 32, WC = 4 / WR, CW = C / WC, NT = CW / 32, VS = C + 4;
   static_assert(NT >= 1, "tile");
@@ -227,7 +230,7 @@ __global__ __launch_bounds__(256) void tok_attn_out_kernel(const TokParams P) {
 
   floatx16 acc[NT];
   // av = ao Wo^T + bo + LN1(x)   (models/unet_cond.py:49-50)
-  tok_gemm<C, NT>(Ah, Al, P.w0, nw, acc, arow0, fr, fh);
+  tok_gemm<C, NT, X1>(Ah, Al, P.w0, nw, acc, arow0, fr, fh);
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     const int col = nw + 32 * j + fr;
@@ -244,7 +247,7 @@ __global__ __launch_bounds__(256) void tok_attn_out_kernel(const TokParams P) {
   tok_rows<C, TM, ROWS_LN>(&Av[0][0], VS, 0, TM, P.l2w, P.l2b, Ah, Al, nullptr, nullptr);
   __syncthreads();
   // f = GELU(LN2(av) W1^T + b1)  (ff_self[1:3])
-  tok_gemm<C, NT>(Ah, Al, P.w1, nw, acc, arow0, fr, fh);
+  tok_gemm<C, NT, X1>(Ah, Al, P.w1, nw, acc, arow0, fr, fh);
   __syncthreads();  // every wave is done reading the LN2 planes
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
@@ -261,7 +264,7 @@ __global__ __launch_bounds__(256) void tok_attn_out_kernel(const TokParams P) {
   }
   __syncthreads();
   // out = f W2^T + b2 + av  (ff_self[3] + residual, models/unet_cond.py:51)
-  tok_gemm<C, NT>(Ah, Al, P.w2, nw, acc, arow0, fr, fh);
+  tok_gemm<C, NT, X1>(Ah, Al, P.w2, nw, acc, arow0, fr, fh);
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     const int col = nw + 32 * j + fr;

@@ -102,11 +102,12 @@ class NativeModel:
         if env:
             self.set_precision(env)
 
-    PRECISIONS = {"fp32": 0, "x3": 1}
+    PRECISIONS = {"fp32": 0, "x3": 1, "f16": 2}
 
     def set_precision(self, prec) -> None:
-        """GEMM arithmetic: "x3" (default; fp32 split into fp16 hi+lo, 3 MFMAs, fp32 accumulate)
-        or "fp32" (fp32 MFMA, exact fp32 products)."""
+        """GEMM arithmetic: "x3" (default; fp32 split into fp16 hi+lo, 3 MFMAs, fp32 accumulate),
+        "fp32" (fp32 MFMA, exact fp32 products) or "f16" (BASELINE config 4: GEMM / attention
+        operands rounded to fp16, one MFMA, fp32 accumulate; norms, softmax and the scheduler stay fp32)."""
         code = self.PRECISIONS[prec] if isinstance(prec, str) else int(prec)
         check(self.lib.dmx_model_set_precision(self.handle, code))
 

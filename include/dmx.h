@@ -70,7 +70,8 @@ int dmx_model_set_tensor(dmx_model* m, const char* name, const float* dev_ptr, c
 /* Repack every registered tensor into the model's kernel layouts (device-side). */
 int dmx_model_finalize(dmx_model* m, void* stream);
 /* GEMM arithmetic: 0 = fp32 MFMA (exact fp32 products), 1 (default) = fp32 operands split
- * into fp16 hi+lo on the fp16 matrix cores (3 MFMAs, fp32 accumulate, ~1e-7 relative). */
+ * into fp16 hi+lo on the fp16 matrix cores (3 MFMAs, fp32 accumulate, ~1e-7 relative),
+ * 2 = fp16 operands (BASELINE config 4: one MFMA, fp32 accumulate, fp32 norms/softmax/scheduler). */
 int dmx_model_set_precision(dmx_model* m, int prec);
 int dmx_model_get_precision(const dmx_model* m);
 
