@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=3, help="oracle steps timed for cpu_baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--config5-steps", type=int, default=100,
+                    help="steps timed in BASELINE config 5 (B=1, VAE decode of every x_t) (0 = skip)")
     ap.add_argument("--config4-steps", type=int, default=100,
                     help="steps timed in BASELINE config 4 (fp16 arithmetic) beside the headline (0 = skip)")
     return ap.parse_args()
@@ -169,6 +171,40 @@ def roofline(records, pmc=None):
     return rl, agg
 
 
+def config5(nm, args, tables, seed):
+    """BASELINE config 5 (generate_steps.py:158-187): B=1, and before every denoise_cond the
+    current latent x_t is decoded by the frozen VAE to a 256x256 uint8 image (the PNG write
+    itself is host I/O, excluded).  Per step: one VAE decode launch sequence + one CFG step
+    (replayed hipGraph); units = denoising steps/s with per-step decode."""
+    from dmx import synth
+    from models.vae import VAE
+    dev = torch.device("cuda", torch.cuda.current_device())
+    vae = VAE()
+    vae.load_state_dict(synth.vae_weights(1))
+    vae = vae.to(dev).eval()
+    vn = vae.native()
+    x, y, vals, mask = make_inputs(1, args.hw, dev, seed=5)
+    t_dev = torch.full((1,), args.T, dtype=torch.long, device=dev)
+
+    def run(k):
+        for _ in range(k):
+            vn.decode(x, want_img=False, want_u8=True)
+            nm.sample_loop(x, t_dev, y, 0, vals, mask, args.guidance, tables, 1, seed=seed)
+
+    run(5)
+    torch.cuda.synchronize()
+    t_dev.fill_(args.T)
+    t0 = time.perf_counter()
+    run(args.config5_steps)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    assert torch.isfinite(x).all(), "non-finite latents (config 5)"
+    return {"workload": "config 5: generate_steps path, B=1, VAE decode (uint8 256x256) of x_t before every CFG step",
+            "value": round(args.config5_steps / dt, 2), "unit": "denoising steps/s (B=1, decode every step)",
+            "ms_per_step": round(dt / args.config5_steps * 1e3, 4), "steps": args.config5_steps, "dtype": "f32 (x3)",
+            "gflop_per_step": round(2 * UNET_GFLOP_PER_SAMPLE + 11.52, 2)}
+
+
 def config4(nm, x, y, vals, mask, args, tables, seed):
     """BASELINE config 4: the same CFG step with fp16 GEMM/attention operands (one f16 MFMA,
     fp32 accumulate, fp32 norms/softmax/scheduler); tolerance study in tests/test_gpu_f16.py.
@@ -261,6 +297,8 @@ def main():
     }
     if world == 1 and args.config4_steps > 0:
         out["config4"] = config4(nm, x, y, vals, mask, args, tables, seed)
+    if world == 1 and args.config5_steps > 0:
+        out["config5"] = config5(nm, args, tables, seed)
     if rank == 0:
         if not args.no_profile:
             xp = x.clone()
