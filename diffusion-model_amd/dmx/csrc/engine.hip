@@ -939,7 +939,11 @@ static float* attn_block_fused(Run& R, const AttnW& a, const float* x, int N, in
       const char* e = std::getenv("DMX_TOK_NB64");
       return e ? std::atoi(e) : 192;
     }();
-    const int nb = C == 64 ? nb64 : 128;  // output columns per block (grid.y = 3C / nb)
+    static const int nb256 = [] {  // C = 256: 64 columns per block doubles the grid (M <= 8192 here)
+      const char* e = std::getenv("DMX_TOK_NB256");
+      return e ? std::atoi(e) : 64;
+    }();
+    const int nb = C == 64 ? nb64 : C == 256 ? nb256 : 128;  // output columns per block (grid.y = 3C / nb)
     const dim3 grid(cdiv(M, 64), 3 * C / nb);
     const int x1 = R.m->prec == 2 ? 1 : 0;
     R.begin("tok_ln_qkv_kernel<" + cs + ", " + std::to_string(nb) + ", " + std::to_string(x1) + ">",
@@ -952,7 +956,10 @@ static float* attn_block_fused(Run& R, const AttnW& a, const float* x, int N, in
         else TQ(64, 64);
         break;
       case 128: TQ(128, 128); break;
-      default: TQ(256, 128); break;
+      default:
+        if (nb == 64) TQ(256, 64);
+        else TQ(256, 128);
+        break;
     }
 #undef TQ
     R.end();
@@ -976,7 +983,13 @@ static float* attn_block_fused(Run& R, const AttnW& a, const float* x, int N, in
     const int tm = C == 64 ? 64 : (C == 256 || cdiv(M, 64) < 512) ? 32 : 64;
     const int blocks = cdiv(M, tm);
     const int x1 = R.m->prec == 2 ? 1 : 0;
-    R.begin("tok_attn_out_kernel<" + std::to_string(C) + ", " + std::to_string(tm) + ", " + std::to_string(x1) + ">",
+    static const int nw256 = [] {  // C = 256: 8 waves per 32-token tile (one 32-column tile each)
+      const char* e = std::getenv("DMX_TOK_NW256");
+      return e ? std::atoi(e) : 8;
+    }();
+    const int nw = C == 256 ? nw256 : 4;
+    R.begin("tok_attn_out_kernel<" + std::to_string(C) + ", " + std::to_string(tm) + ", " + std::to_string(x1) +
+                ", " + std::to_string(nw) + ">",
             6.0 * M * (double)C * C,
             12.0 * (double)M * C);
 #define TB(CC, TT) (x1 ? tok_attn_out_kernel<CC, TT, 1><<<blocks, 256, 0, R.st>>>(tp) \
@@ -984,7 +997,10 @@ static float* attn_block_fused(Run& R, const AttnW& a, const float* x, int N, in
     if (C == 64) TB(64, 64);
     else if (C == 128 && tm == 64) TB(128, 64);
     else if (C == 128) TB(128, 32);
-    else TB(256, 32);
+    else if (nw == 8) {
+      if (x1) tok_attn_out_kernel<256, 32, 1, 8><<<blocks, 512, 0, R.st>>>(tp);
+      else tok_attn_out_kernel<256, 32, 0, 8><<<blocks, 512, 0, R.st>>>(tp);
+    } else TB(256, 32);
 #undef TB
     R.end();
     HIPCHK(hipGetLastError());

@@ -66,10 +66,10 @@ DMX_DEV float group_sum(float s) {
 // load instruction covers 16G contiguous bytes of a row); every load of the pass is issued
 // before any is used.  LN = nn.LayerNorm: two-pass mean / biased variance, eps 1e-5, the
 // same per-element expression as layernorm_kernel.
-template <int C, int TM, int MODE>
+template <int C, int TM, int MODE, int NW = 4>
 DMX_DEV void tok_rows(const float* src, int ld, int m0, int M, const float* g, const float* b,
                       _Float16 (*Ah)[C + 8], _Float16 (*Al)[C + 8], float* mu, float* rs) {
-  constexpr int G = C / 16, RP = 64 / G, RW = TM / 4, NP = RW / RP;
+  constexpr int G = C / 16, RP = 64 / G, RW = TM / NW, NP = RW / RP;
   static_assert(G == 4 || G == 8 || G == 16, "C");
   static_assert(NP >= 1 && RW % RP == 0, "rows per wave");
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -211,10 +211,10 @@ __global__ __launch_bounds__(256) void tok_ln_qkv_kernel(const TokParams P) {
 }
 
 // TB: out-proj + residual, LN2, FF1 + GELU, FF2 + residual for TM tokens x all C channels.
-// TM = 64: waves 2 (rows) x 2 (cols); TM = 32: 1 x 4 (more blocks for small M / wide C).
-template <int C, int TM, int X1 = 0>
-__global__ __launch_bounds__(256) void tok_attn_out_kernel(const TokParams P) {
-  constexpr int WR = TM / 32, WC = 4 / WR, CW = C / WC, NT = CW / 32, VS = C + 4;
+// NW waves: TM = 64: 2 (rows) x NW/2 (cols); TM = 32: 1 x NW (more blocks for small M / wide C).
+template <int C, int TM, int X1 = 0, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void tok_attn_out_kernel(const TokParams P) {
+  constexpr int WR = TM / 32, WC = NW / WR, CW = C / WC, NT = CW / 32, VS = C + 4;
   static_assert(NT >= 1, "tile");
   __shared__ __attribute__((aligned(16))) _Float16 Ah[TM][C + 8];
   __shared__ __attribute__((aligned(16))) _Float16 Al[TM][C + 8];
@@ -224,8 +224,8 @@ __global__ __launch_bounds__(256) void tok_attn_out_kernel(const TokParams P) {
   const int wm = wid / WC, wn = wid % WC, m0 = blockIdx.x * TM;
   const int M = P.M, nw = wn * CW, arow0 = wm * 32;
 
-  tok_rows<C, TM, ROWS_SPLIT>(P.ao, C, m0, M, nullptr, nullptr, Ah, Al, nullptr, nullptr);
-  tok_rows<C, TM, ROWS_STATS>(P.x, C, m0, M, nullptr, nullptr, Ah, Al, mu1, rs1);
+  tok_rows<C, TM, ROWS_SPLIT, NW>(P.ao, C, m0, M, nullptr, nullptr, Ah, Al, nullptr, nullptr);
+  tok_rows<C, TM, ROWS_STATS, NW>(P.x, C, m0, M, nullptr, nullptr, Ah, Al, mu1, rs1);
   __syncthreads();
 
   floatx16 acc[NT];
@@ -244,7 +244,7 @@ __global__ __launch_bounds__(256) void tok_attn_out_kernel(const TokParams P) {
   }
   __syncthreads();
   // LN2(av) -> A planes (ff_self[0])
-  tok_rows<C, TM, ROWS_LN>(&Av[0][0], VS, 0, TM, P.l2w, P.l2b, Ah, Al, nullptr, nullptr);
+  tok_rows<C, TM, ROWS_LN, NW>(&Av[0][0], VS, 0, TM, P.l2w, P.l2b, Ah, Al, nullptr, nullptr);
   __syncthreads();
   // f = GELU(LN2(av) W1^T + b1)  (ff_self[1:3])
   tok_gemm<C, NT, X1>(Ah, Al, P.w1, nw, acc, arow0, fr, fh);
