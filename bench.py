@@ -209,6 +209,7 @@ def config4(nm, x, y, vals, mask, args, tables, seed):
     """BASELINE config 4: the same CFG step with fp16 GEMM/attention operands (one f16 MFMA,
     fp32 accumulate, fp32 norms/softmax/scheduler); tolerance study in tests/test_gpu_f16.py.
     Reported beside the headline, never as `value` (reduced precision)."""
+    old = nm.precision
     nm.set_precision("f16")
     try:
         xs = x.clone()
@@ -222,7 +223,7 @@ def config4(nm, x, y, vals, mask, args, tables, seed):
         dt = time.perf_counter() - t0
         assert torch.isfinite(xs).all(), "non-finite latents (config 4)"
     finally:
-        nm.set_precision("x3")
+        nm.set_precision(old)
     return {"workload": "config 4: config 2 with fp16 weights/activations, fp32 accumulate + scheduler",
             "value": round(args.config4_steps / dt, 3), "unit": "CFG batch-steps/s (B=%d)" % args.batch,
             "ms_per_step": round(dt / args.config4_steps * 1e3, 4), "steps": args.config4_steps, "dtype": "f16",
