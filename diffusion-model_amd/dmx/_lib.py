@@ -76,6 +76,7 @@ SIGNATURES = [
     ("dmx_ddpm_update", _I, [_P, _P, _P, _P, ctypes.c_float, _P, _I, _P, _P, _P, _I, _P, ctypes.c_uint64, _I64,
                              _I, _I, _I, _I, _P]),
     ("dmx_vae_decode", _I, [_P, _P, _P, _P, _I, _I, _I, _P]),
+    ("dmx_vae_encode", _I, [_P, _P, _P, _P, _P, _I, _I, _I, _P]),
     ("dmx_model_workspace_bytes", _I64, [_P]),
     ("dmx_debug_enable", _I, [_P, _I]),
     ("dmx_debug_num_taps", _I, [_P]),

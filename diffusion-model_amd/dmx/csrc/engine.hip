@@ -233,6 +233,10 @@ struct dmx_model {
   // VAE decoder
   dmx::ConvW vconv[4], vconvt[3];
   dmx::Vec vg[6], vb[6];
+  // VAE encoder (conv3x3 / conv4x4-s2 implicit GEMMs, GN(8) affine, 1x1 heads as raw fp32)
+  dmx::ConvW venc[6];
+  dmx::Vec veg[6], veb[6];
+  float *wmu = nullptr, *bmu = nullptr, *wlv = nullptr, *blv = nullptr;
   // workspace + graph
   dmx::Arena ws;
   void* ws_mem = nullptr;
@@ -418,6 +422,18 @@ static void finalize_model(dmx_model* m, hipStream_t st) {
     }
     m->vconv[3].B = P.copy("dec.18.weight");
     m->vconv[3].bias = P.copy("dec.18.bias");
+    // encoder (models/vae.py:17-30): conv3x3 s1 and conv4x4 s2 alternating, GN(8) + GELU after each
+    const int eci[6] = {3, 64, 64, 128, 128, 256}, eco[6] = {64, 64, 128, 128, 256, 256};
+    for (int i = 0; i < 6; ++i) {
+      const std::string w = "enc." + std::to_string(3 * i);
+      m->venc[i] = P.conv(w + ".weight", w + ".bias", eci[i], eco[i], (i & 1) ? 4 : 3, i == 0 ? 4 : 0);
+      m->veg[i] = P.vec("enc." + std::to_string(3 * i + 1) + ".weight");
+      m->veb[i] = P.vec("enc." + std::to_string(3 * i + 1) + ".bias");
+    }
+    m->wmu = P.copy("to_mu.weight");
+    m->bmu = P.copy("to_mu.bias");
+    m->wlv = P.copy("to_logvar.weight");
+    m->blv = P.copy("to_logvar.bias");
   } else {
     const bool cond = m->kind != DMX_UNET;
     const int cin_pad = rup(m->in_ch, 4);
@@ -672,7 +688,9 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   p.W = W;
   p.M = M;
   p.taps = cw.taps;
-  p.geom = cw.phases == 4 ? 2 : (cw.taps == 9 ? 1 : 0);
+  p.geom = cw.phases == 4 ? 2 : (cw.taps == 9 ? 1 : (cw.taps == 16 ? 3 : 0));
+  p.Hin = p.geom == 3 ? 2 * H : H;  // geom 3 (4x4 / s2 conv): H x W is the output grid
+  p.Win = p.geom == 3 ? 2 * W : W;
   p.Kreal = cw.taps * cw.cin;
   p.Kpad = cw.kpad;
   p.Cout = cw.cout;
@@ -705,7 +723,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   const int x3_nbuf = (x1 || x3_pipe() == 1 || x3_pipe() == 2) ? 1 : 2, x3_sa = ash != nullptr ? 1 : 0;
   const int creal = (src_mode == SRC_NCHW && s.C0) ? s.C0 : cw.cin;
   const double flops = 2.0 * (double)M * cw.phases * cw.cout * (double)cw.taps * creal;
-  const double bytes = 4.0 * ((double)M * cw.phases * cw.cout + (double)M * s.C +
+  const double bytes = 4.0 * ((double)M * cw.phases * cw.cout + (double)N * p.Hin * p.Win * s.C +
                               (double)cw.phases * cw.cout * cw.taps * cw.cin);
   char nm[96];
   if (splits > 1) {
@@ -1301,6 +1319,50 @@ static void vae_body(Run& R, const float* z, float* img, uint8_t* u8, int n, int
   HIPCHK(hipGetLastError());
 }
 
+// VAE encoder (models/vae.py:17-30, 51-62) on n images (n,3,h,w), h, w multiples of 8:
+// [conv3x3 | conv4x4-s2 GEMM] (+row stats) -> GN(8) finalize -> GN+GELU materialised, x6, then
+// the 1x1 mu / logvar heads + reparameterisation + per-sample KL in vae_enc_tail_kernel.
+static void vae_enc_body(Run& R, const float* x, const float* eps, float* z, float* kl, int n, int h, int w) {
+  dmx_model* m = R.m;
+  const int G = 8;
+  SrcDesc s = plain_src(x, 4);  // NCHW image, 3 real channels padded to 4
+  s.C0 = 3;
+  int mode = SRC_NCHW;
+  int H = h, W = w;
+  const float* act = nullptr;
+  for (int stage = 0; stage < 6; ++stage) {
+    const bool strided = stage & 1;
+    const ConvW& cw = m->venc[stage];
+    const int Ho = strided ? H / 2 : H, Wo = strided ? W / 2 : W;
+    const int Mo = n * Ho * Wo;
+    const int seg = std::min(32, cw.cout / G);
+    R.layer = "enc" + std::to_string(stage);
+    float* r = R.ws.get<float>((size_t)Mo * cw.cout);
+    float2* rp = R.ws.get<float2>((size_t)Mo * (cw.cout / seg));
+    float2* st = R.ws.get<float2>((size_t)n * G);
+    float* a = R.ws.get<float>((size_t)Mo * cw.cout);
+    const int rr = gemm(R, s, mode, n, Ho, Wo, cw, EPI_STATS, r, nullptr, rp, seg);  // rows = output pixels
+    gn_finalize(R, rp, st, n, rr, cw.cout / seg, G, cw.cout, Ho * Wo);
+    NormParams np = norm_params(r, nullptr, 0, 0, m->veg[stage].p, m->veb[stage].p, cw.cout, Ho * Wo, a);
+    np.stats = st;
+    np.G = G;
+    np.act = 1;
+    norm(R, np, n);
+    R.tap(R.layer, a, (size_t)Mo * cw.cout);
+    act = a;
+    s = plain_src(a, cw.cout);
+    mode = SRC_PLAIN;
+    H = Ho;
+    W = Wo;
+  }
+  if (R.plan) return;
+  R.begin("vae_enc_tail_kernel", 2.0 * n * H * W * 8 * 256, 4.0 * (double)n * H * W * (256 + 4 + 4));
+  vae_enc_tail_kernel<<<n, 256, 0, R.st>>>(act, m->wmu, m->bmu, m->wlv, m->blv, eps, z, kl, H * W, 0.18215f,
+                                            1.0f / ((float)h * (float)w));
+  R.end();
+  HIPCHK(hipGetLastError());
+}
+
 }  // namespace dmx
 
 // ===========================================================================
@@ -1646,6 +1708,27 @@ int dmx_vae_decode(dmx_model* m, const float* z, float* img, uint8_t* u8, int n,
       run_planned(m, st, [&](Run& R) {
         vae_body(R, z + (size_t)s * 4 * h * w, img ? img + (size_t)s * 3 * 64 * h * w : nullptr,
                  u8 ? u8 + (size_t)s * 64 * h * w * 3 : nullptr, b, h, w);
+      });
+    }
+  });
+}
+
+int dmx_vae_encode(dmx_model* m, const float* x, const float* eps, float* z, float* kl, int n, int h, int w,
+                   void* stream) {
+  return guarded([&] {
+    REQUIRE(m != nullptr, "null model");
+    if (!m->finalized) throw Error(DMX_E_STATE, "model weights not finalized");
+    REQUIRE(m->kind == DMX_VAE, "not a VAE model");
+    REQUIRE(x && eps && z && kl, "null tensor");
+    REQUIRE(n >= 1 && h >= 8 && w >= 8 && h % 8 == 0 && w % 8 == 0, "image sides must be multiples of 8");
+    const int chunk = 16;  // bounds workspace
+    const int hl = h / 8, wl = w / 8;
+    hipStream_t st = (hipStream_t)stream;
+    for (int s = 0; s < n; s += chunk) {
+      const int b = std::min(chunk, n - s);
+      run_planned(m, st, [&](Run& R) {
+        vae_enc_body(R, x + (size_t)s * 3 * h * w, eps + (size_t)s * 4 * hl * wl, z + (size_t)s * 4 * hl * wl,
+                     kl + s, b, h, w);
       });
     }
   });

@@ -27,7 +27,9 @@ struct IgemmParams {
   int H, W;           // GEMM row grid (input grid of the conv / token grid)
   int M;              // rows = N * H * W
   int taps;
-  int geom;           // 0: linear (1 tap), 1: conv3x3 pad 1, 2: ConvTranspose 4x4/s2 phase (4 taps)
+  int geom;           // 0: linear (1 tap), 1: conv3x3 pad 1, 2: ConvTranspose 4x4/s2 phase (4 taps),
+                      // 3: Conv2d 4x4 / stride 2 / pad 1 (16 taps; rows = output pixels)
+  int Hin, Win;       // source map (== H, W except geom 3: 2H, 2W)
   int Kreal, Kpad;
   int Cout, Npad;
   int osy, osx;       // output stride (2 for ConvT phases)
@@ -57,9 +59,20 @@ DMX_DEV void tap_offset(int geom, int phase, int tap, int& dy, int& dx) {
     const int jy = tap >> 1, jx = tap & 1;
     dy = (phase >> 1) ? 1 - jy : -jy;
     dx = (phase & 1) ? 1 - jx : -jx;
+  } else if (geom == 3) {  // tap = ky * 4 + kx; input (2y + ky - 1, 2x + kx - 1)
+    dy = (tap >> 2) - 1;
+    dx = (tap & 3) - 1;
   } else {
     dy = dx = 0;
   }
+}
+
+// Source-map pixel index of GEMM row m's tap origin (geom 3: the stride-2 anchor (2y, 2x) in
+// the Hin x Win input; otherwise the row's own pixel).
+DMX_DEV int row_anchor(int geom, int m, int H, int W, int Hin, int Win) {
+  if (geom != 3) return m;
+  const int HW = H * W, n = m / HW, r = m - n * HW, y = r / W, x = r - y * W;
+  return (n * Hin + 2 * y) * Win + 2 * x;
 }
 
 // XCD-aware tile order (cdna_hip_programming.md T1): hardware deals consecutive block ids
@@ -68,10 +81,22 @@ DMX_DEV void tap_offset(int geom, int phase, int tap, int& dy, int& dx) {
 // the same input rows (3x3 taps) then share one L2.  Bijective for any grid size.
 // Bitmask of the taps whose input pixel of output row m is inside the H x W map
 // (bit t = tap t of the GEMM geometry; 0 for m >= M).
-DMX_DEV unsigned tap_mask(int geom, int phase, int taps, int m, int M, int H, int W) {
+DMX_DEV unsigned tap_mask(int geom, int phase, int taps, int m, int M, int H, int W, int Hin = 0, int Win = 0) {
   if (m >= M) return 0u;
   if (geom == 0) return 1u;
   const int HW = H * W, n = m / HW, r = m - n * HW, y = r / W, x = r - y * W;
+  if (geom == 3) {  // 4x4 / s2 / p1: rows and columns 2y-1 .. 2y+2 of the Hin x Win input
+    unsigned ry = 0u, cx = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      ry |= (2 * y + k - 1 >= 0 && 2 * y + k - 1 < Hin) ? 1u << k : 0u;
+      cx |= (2 * x + k - 1 >= 0 && 2 * x + k - 1 < Win) ? 1u << k : 0u;
+    }
+    unsigned mk = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) mk |= ((ry >> k) & 1u) ? cx << (4 * k) : 0u;
+    return mk;
+  }
   if (geom == 1) {  // 3x3, pad 1: outer product of row / column validity
     const unsigned ry = (y > 0 ? 1u : 0u) | 2u | (y < H - 1 ? 4u : 0u);
     const unsigned cx = (x > 0 ? 1u : 0u) | 2u | (x < W - 1 ? 4u : 0u);
@@ -285,6 +310,10 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(const IgemmParams p) {
     const int r = mm - an[i] * HW;
     ay[i] = r / p.W;
     ax[i] = r - ay[i] * p.W;
+    if (p.geom == 3) {  // stride-2 anchor in the source map
+      ay[i] *= 2;
+      ax[i] *= 2;
+    }
   }
 
   floatx4 ra[AP], rb[BP];
@@ -298,8 +327,8 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(const IgemmParams p) {
 #pragma unroll
     for (int i = 0; i < AP; ++i) {
       const int iy = ay[i] + ddy, ix = ax[i] + ddx;
-      const bool ok = kv && av[i] && iy >= 0 && ix >= 0 && iy < p.H && ix < p.W;
-      ra[i] = ok ? load_src4<SRC>(p.src, an[i], iy, ix, c, p.H, p.W) : floatx4{0.f, 0.f, 0.f, 0.f};
+      const bool ok = kv && av[i] && iy >= 0 && ix >= 0 && iy < p.Hin && ix < p.Win;
+      ra[i] = ok ? load_src4<SRC>(p.src, an[i], iy, ix, c, p.Hin, p.Win) : floatx4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int i = 0; i < BP; ++i)

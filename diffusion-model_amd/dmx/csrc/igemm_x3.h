@@ -82,8 +82,8 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
 #pragma unroll
   for (int i = 0; i < AP; ++i) {
     const int m = m0 + ra + i * ARS;
-    rpix[i] = m < p.M ? m : 0;
-    tmask[i] = tap_mask(p.geom, phase, p.taps, m, p.M, p.H, p.W);
+    rpix[i] = m < p.M ? row_anchor(p.geom, m, p.H, p.W, p.Hin, p.Win) : 0;
+    tmask[i] = tap_mask(p.geom, phase, p.taps, m, p.M, p.H, p.W, p.Hin, p.Win);
   }
 
   floatx4 ra4[SPLIT_A ? 1 : AP];
@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
   auto load_tile = [&](int kt) {
     int ddy, ddx;
     tap_offset(p.geom, phase, ltap, ddy, ddx);
-    const int delta = ddy * p.W + ddx;
+    const int delta = ddy * p.Win + ddx;
     const int tap = ltap, c = lc;
     lc += BK;
     if (lc >= C) {
@@ -282,8 +282,8 @@ __global__ __launch_bounds__(256) void igemm_x3g_kernel(const X3Params P) {
     const int row = wid * (BM / 4) + 16 * q + lr;
     achunk[q] = lj ^ ((row >> 2) & 3);
     const int m = m0 + row;
-    rpix[q] = m < p.M ? m : 0;
-    tmask[q] = tap_mask(p.geom, phase, p.taps, m, p.M, p.H, p.W);
+    rpix[q] = m < p.M ? row_anchor(p.geom, m, p.H, p.W, p.Hin, p.Win) : 0;
+    tmask[q] = tap_mask(p.geom, phase, p.taps, m, p.M, p.H, p.W, p.Hin, p.Win);
   }
   size_t brow[BQ];  // element offset of this lane's B chunk in the [Npad][Kpad] planes (k-tile 0)
 #pragma unroll
@@ -305,7 +305,7 @@ __global__ __launch_bounds__(256) void igemm_x3g_kernel(const X3Params P) {
       int dy, dx;
       tap_offset(p.geom, phase, tap, dy, dx);
       const bool ok = tap < 32 && ((tmask[q] >> tap) & 1u);
-      const int off = (rpix[q] + dy * p.W + dx) * C + c;
+      const int off = (rpix[q] + dy * p.Win + dx) * C + c;
       const void* gh = ok ? (const void*)(P.Ash + off) : (const void*)g_zero16;
       const void* gl = ok ? (const void*)(P.Asl + off) : (const void*)g_zero16;
       const int rb = (wid * (BM / 4) + 16 * q) * ROWB;

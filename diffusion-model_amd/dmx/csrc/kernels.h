@@ -618,6 +618,53 @@ __global__ __launch_bounds__(256) void vae_tail_kernel(const float* in, const fl
   }
 }
 
+// VAE encoder tail (models/vae.py:52-60): to_mu / to_logvar (1x1 convs 256 -> 4, bias),
+// logvar.clamp(-30, 20), std = exp(0.5 logvar), z = (mu + eps * std) * scale with eps the
+// reference's randn_like draw (passed in, NCHW), and the per-sample KL term
+// 0.5 * sum_{c,y,x}(exp(lv) + mu^2 - 1 - lv) / (H_img * W_img).  One block per sample; the KL
+// sum is reduced in a fixed order (per-thread strided partials, then a fixed tree).
+// in: materialised GELU(GN(enc.15)) NHWC [N][HW][256].
+__global__ __launch_bounds__(256) void vae_enc_tail_kernel(const float* in, const float* wmu, const float* bmu,
+                                                           const float* wlv, const float* blv, const float* eps,
+                                                           float* z, float* kl, int HW, float scale, float inv_px) {
+  __shared__ float ws[8][256];  // rows 0-3: to_mu, 4-7: to_logvar ([out][in] of the 1x1 convs)
+  __shared__ float red[256];
+  for (int i = threadIdx.x; i < 8 * 256; i += 256) ws[i / 256][i % 256] = i < 1024 ? wmu[i] : wlv[i - 1024];
+  __syncthreads();
+  const int n = blockIdx.x;
+  float kacc = 0.f;
+  for (int pix = threadIdx.x; pix < HW; pix += 256) {
+    const float* src = in + ((size_t)n * HW + pix) * 256;
+    float a[8];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      a[o] = bmu[o];
+      a[o + 4] = blv[o];
+    }
+    for (int c = 0; c < 256; c += 4) {
+      const floatx4 v = ld4(src + c);
+#pragma unroll
+      for (int o = 0; o < 8; ++o)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[o] += v[j] * ws[o][c + j];
+    }
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      const float mu = a[o], lv = fminf(fmaxf(a[o + 4], -30.f), 20.f);
+      const size_t idx = ((size_t)n * 4 + o) * HW + pix;
+      z[idx] = (mu + eps[idx] * expf(0.5f * lv)) * scale;
+      kacc += ((expf(lv) + mu * mu) - 1.f) - lv;
+    }
+  }
+  red[threadIdx.x] = kacc;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) kl[n] = 0.5f * red[0] * inv_px;
+}
+
 // Weight repack into the implicit-GEMM B layout [phase][Npad][Kpad] (zero pad).
 //   kind 0: Conv2d [Cout][Cin][KS][KS], k = (ky*KS+kx)*Cin + c
 //   kind 1: Linear [Cout][Cin],        k = c

@@ -236,6 +236,18 @@ class NativeModel:
                                           ctypes.c_void_p(_stream(z.device))))
         return img, u8
 
+    def encode(self, x, eps) -> Tuple[torch.Tensor, torch.Tensor]:
+        """x (n,3,h,w), eps (n,4,h/8,w/8) -> (z, per-sample KL (n,)) (models/vae.py:51-62)."""
+        n, c, h, w = x.shape
+        x = x.contiguous().float()
+        eps = eps.contiguous().float()
+        z = torch.empty((n, 4, h // 8, w // 8), device=x.device, dtype=torch.float32)
+        kl = torch.empty((n,), device=x.device, dtype=torch.float32)
+        with torch.cuda.device(x.device):
+            check(self.lib.dmx_vae_encode(self.handle, _ptr(x), _ptr(eps), _ptr(z), _ptr(kl), n, h, w,
+                                          ctypes.c_void_p(_stream(x.device))))
+        return z, kl
+
 
 def ddpm_update(x, eu, ec, guidance, t, tables, noise=None, seed=0, sample_offset=0):
     """Standalone K1 (diff.py:151,158-162) for duck-typed models: returns x'."""

@@ -4,15 +4,15 @@
 (conv3x3 / 4-phase ConvTranspose implicit GEMMs, GroupNorm(8)+GELU fused into
 the next layer's operand load, sigmoid + uint8 quantisation in the last kernel).
 
-``encode`` is not on the denoising hot path (SURVEY.md §8f, rank 1 "next"): the
-sampler only uses it on a zero dummy to infer the latent shape, which
-``diff.Diffuser`` does analytically (replaying its RNG draw).  It is provided here
-with plain torch ops so that the class stays API-complete; it is NOT a native path.
+``encode`` (SURVEY.md §8f, rank 1 "next") runs natively too (dmx_vae_encode:
+conv3x3 / conv4x4-stride-2 implicit GEMMs, GroupNorm(8)+GELU, then mu / logvar heads,
+reparameterisation and the KL term in one tail kernel).  The sampler itself only needs
+the latent shape of a zero dummy, which ``diff.Diffuser`` derives analytically while
+replaying the encoder's RNG draw.
 """
 from __future__ import annotations
 
 import torch
-import torch.nn.functional as F
 
 from dmx import _lib, spec
 from models._native import NativeBacked, build_param_tree
@@ -48,20 +48,16 @@ class VAE(NativeBacked):
         _, u8 = self.native().decode(z, want_img=False, want_u8=True)
         return u8
 
-    # ---- off the hot path (torch ops) -------------------------------------------------------
     def encode(self, x: torch.Tensor):
-        """models/vae.py:51-62 (consumes one randn_like draw like the reference)."""
-        sd = dict(self.named_parameters())
-        h = x
-        for i, k in ((0, 3), (3, 4), (6, 3), (9, 4), (12, 3), (15, 4)):
-            stride, pad = (1, 1) if k == 3 else (2, 1)
-            h = F.conv2d(h, sd[f"enc.{i}.weight"], sd[f"enc.{i}.bias"], stride, pad)
-            h = F.gelu(F.group_norm(h, 8, sd[f"enc.{i + 1}.weight"], sd[f"enc.{i + 1}.bias"], 1e-5))
-        mu = F.conv2d(h, sd["to_mu.weight"], sd["to_mu.bias"])
-        logvar = F.conv2d(h, sd["to_logvar.weight"], sd["to_logvar.bias"]).clamp(-30.0, 20.0)
-        std = torch.exp(0.5 * logvar)
-        z = (mu + torch.randn_like(std) * std) * self.scale_factor
-        kl = 0.5 * torch.sum(torch.exp(logvar) + mu ** 2 - 1.0 - logvar, dim=(1, 2, 3)) / (x.size(2) * x.size(3))
+        """models/vae.py:51-62 -> (z, kl.mean()), natively (dmx_vae_encode: conv3x3 / conv4x4-s2
+        implicit GEMMs + GN(8)+GELU, then the mu / logvar heads, reparameterisation and KL in one
+        tail kernel).  The randn_like(std) draw is made here with torch on x's device, so the
+        global RNG stream advances exactly as in the reference.  Image sides must be multiples
+        of 8 (the three stride-2 convs halve them exactly)."""
+        n, _, h, w = x.shape
+        hl, wl = latent_hw(h, w)
+        eps = torch.randn((n, self.z_channels, hl, wl), device=x.device, dtype=torch.float32)
+        z, kl = self.native().encode(x, eps)
         return z, kl.mean()
 
     def forward(self, x):

@@ -123,6 +123,14 @@ int dmx_ddpm_update(const float* x, float* x_out, const float* eu, const float* 
  * z: (n,4,h,w); img: (n,3,8h,8w) fp32 or NULL; u8: (n,8h,8w,3) uint8 (HWC) or NULL. */
 int dmx_vae_decode(dmx_model* m, const float* z, float* img, uint8_t* u8, int n, int h, int w, void* stream);
 
+/* ---- VAE encode (replaces VAE.encode, vae.py:51-62) -------------
+ * x: (n,3,h,w) fp32, h and w multiples of 8; eps: (n,4,h/8,w/8) = the reference's
+ * torch.randn_like(std) draw (caller-drawn, so the global RNG stream matches);
+ * z: (n,4,h/8,w/8) = (mu + eps * exp(0.5 logvar)) * 0.18215; kl: (n,) per-sample KL term
+ * (VAE.encode's returned kl is kl.mean()). */
+int dmx_vae_encode(dmx_model* m, const float* x, const float* eps, float* z, float* kl, int n, int h, int w,
+                   void* stream);
+
 /* ---- measurement: one eager step with a HIP event pair around every launch -----------
  * Fills up to `cap` records (kernel name as rocprofv3 shows it, layer label, algorithmic
  * FLOPs and HBM bytes of that launch, and its event-timed duration in ms). */

@@ -151,6 +151,20 @@ def vae_decode(sd: SD, z: torch.Tensor, scale_factor: float = 0.18215) -> torch.
     return torch.sigmoid(h)
 
 
+def vae_encode(sd: SD, x: torch.Tensor, eps: torch.Tensor, scale_factor: float = 0.18215):
+    """models/vae.py:51-62 (encoder layers 17-30) with the randn_like draw passed in as eps:
+    returns (z, kl.mean(), mu, clamped logvar)."""
+    h = x
+    for i, (stride, pad) in ((0, (1, 1)), (3, (2, 1)), (6, (1, 1)), (9, (2, 1)), (12, (1, 1)), (15, (2, 1))):
+        h = F.conv2d(h, sd[f"enc.{i}.weight"], sd[f"enc.{i}.bias"], stride, pad)
+        h = F.gelu(F.group_norm(h, 8, sd[f"enc.{i + 1}.weight"], sd[f"enc.{i + 1}.bias"], 1e-5))
+    mu = F.conv2d(h, sd["to_mu.weight"], sd["to_mu.bias"])
+    logvar = F.conv2d(h, sd["to_logvar.weight"], sd["to_logvar.bias"]).clamp(-30.0, 20.0)
+    z = (mu + eps * torch.exp(0.5 * logvar)) * scale_factor
+    kl = 0.5 * torch.sum(torch.exp(logvar) + mu ** 2 - 1.0 - logvar, dim=(1, 2, 3)) / (x.size(2) * x.size(3))
+    return z, kl.mean(), mu, logvar
+
+
 def to_uint8(img: torch.Tensor) -> torch.Tensor:
     """diff.py:58-62 — x*255 -> clamp(0,255) -> .to(uint8) (truncation)."""
     return (img * 255).clamp(0, 255).to(torch.uint8)

@@ -106,6 +106,42 @@ def test_vae_decode_golden(golden, vae, cuda):
     assert ok, info
 
 
+@pytest.mark.parametrize("tag", ["64", "56"])
+@pytest.mark.parametrize("vprec", ["x3", "fp32"])
+def test_vae_encode_golden(golden, vae, vae_sd, cuda, tag, vprec):
+    """VAE.encode (models/vae.py:51-62; conv4x4-s2 implicit GEMM) vs the reference's outputs, including
+    its randn_like draw: z rel-L2 <= 2e-5, KL rel <= 2e-5; the global RNG advanced like the reference."""
+    g = golden("vae_encode.npz")
+    nm = vae.native()
+    old = nm.precision
+    nm.set_precision(vprec)
+    try:
+        x = torch.from_numpy(g[f"x{tag}"]).to(cuda)
+        torch.manual_seed(int(g[f"seed{tag}"]))
+        eps = torch.randn(g[f"eps{tag}"].shape).to(cuda)  # the draw the drop-in makes on `cuda`
+        zn, kln = nm.encode(x, eps)
+        exp_z = ref.vae_encode(vae_sd, x.cpu(), eps.cpu())[0]
+        assert rel(zn, exp_z) < TOL
+        eg = torch.from_numpy(g[f"eps{tag}"])
+        zg, klg = nm.encode(x, eg.to(cuda))
+        assert rel(zg, g[f"z{tag}"]) < TOL
+        assert abs(float(klg.mean()) - float(g[f"kl{tag}"])) <= TOL * abs(float(g[f"kl{tag}"]))
+    finally:
+        nm.set_precision(old)
+
+
+def test_vae_encode_dropin_draws_like_reference(vae, cuda):
+    """VAE.encode draws eps with torch on x's device: the RNG state afterwards equals one randn of z's shape."""
+    x = torch.rand((2, 3, 32, 32), generator=torch.Generator().manual_seed(5)).to(cuda)
+    torch.manual_seed(9)
+    z, kl = vae.encode(x)
+    after = torch.randn(3, device=cuda)
+    torch.manual_seed(9)
+    _ = torch.randn((2, 4, 4, 4), device=cuda)
+    assert torch.equal(after, torch.randn(3, device=cuda))
+    assert z.shape == (2, 4, 4, 4) and kl.dim() == 0 and torch.isfinite(z).all()
+
+
 def test_vae_decode_vs_oracle_odd_batch(vae, cuda, vae_sd):
     z = torch.randn((3, 4, 8, 8), generator=torch.Generator().manual_seed(4))
     with torch.no_grad():

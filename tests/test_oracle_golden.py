@@ -4,6 +4,7 @@ import json
 import os
 
 import numpy as np
+import pytest
 import torch
 
 from conftest import GOLDEN
@@ -109,3 +110,14 @@ def test_short_cond_trajectory_T20(golden, unet_sd):
             t = torch.full((2,), i, dtype=torch.long)
             x = ref.cfg_step(unet_sd, x, t, y, a, ab, 3.0, 0, vals, mask, torch.randn(x.shape))
     assert rel(x, g["latent_32"]) < 1e-5
+
+
+@pytest.mark.parametrize("tag", ["64", "56"])
+def test_vae_encode(golden, vae_sd, tag):
+    """VAE.encode (models/vae.py:51-62) vs the reference's own outputs (make_golden_encode.py)."""
+    g = golden("vae_encode.npz")
+    with torch.no_grad():
+        z, kl, mu, lv = ref.vae_encode(vae_sd, torch.from_numpy(g[f"x{tag}"]), torch.from_numpy(g[f"eps{tag}"]))
+    assert torch.equal(z, torch.from_numpy(g[f"z{tag}"]))
+    assert torch.equal(mu, torch.from_numpy(g[f"mu{tag}"]))
+    assert float(kl) == float(g[f"kl{tag}"])
