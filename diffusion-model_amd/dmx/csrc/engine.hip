@@ -16,6 +16,7 @@
 #include "igemm.h"
 #include "igemm_x3.h"
 #include "kernels.h"
+#include "igemm_pp.h"
 #include "tokmlp.h"
 
 namespace dmx {
@@ -664,15 +665,25 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   const int blocks = cdiv(M, bm) * cdiv(cw.cout, bn) * cw.phases;
   const bool x3 = R.m->prec >= 1 && src_mode == SRC_PLAIN && cw.Bh != nullptr;
   const bool x1 = x3 && R.m->prec == 2;  // config-4 fp16: one MFMA on the hi planes
-  const bool x3g = x3 && !x1 && ash != nullptr && glds_enabled() && s.C % 8 == 0;  // LDS-DMA kernel (BK 32)
-  const int bk = x3g ? 32 : x1 ? 64 : x3 ? (x3_pipe() == 2 ? 64 : X3_BK) : IG_BK;
+  static const int pp_min = [] {  // ping-pong 256-row kernel when its grid has at least this many blocks
+    const char* e = std::getenv("DMX_PP_MIN");
+    return e ? std::atoi(e) : 256;
+  }();
+  static const bool pp_sa0 = [] {  // also for fp32 A sources (split while staging)
+    const char* e = std::getenv("DMX_PP_SA0");
+    return e ? std::atoi(e) != 0 : false;
+  }();
+  const bool pp = x3 && epi == EPI_STATS && cw.phases == 1 && pp_min > 0 && s.C >= 32 &&
+                  (ash != nullptr || pp_sa0) && cdiv(M, 256) * cdiv(cw.cout, bn) >= pp_min;
+  const bool x3g = x3 && !pp && !x1 && ash != nullptr && glds_enabled() && s.C % 8 == 0;  // LDS-DMA kernel (BK 32)
+  const int bk = (x3g || pp) ? 32 : x1 ? 64 : x3 ? (x3_pipe() == 2 ? 64 : X3_BK) : IG_BK;
   const int nkt = cw.kpad / bk;
   int splits = 1, ksplit = nkt;
   static const int split_below = [] {  // split K when the grid has fewer blocks than this
     const char* e = std::getenv("DMX_SPLIT_BELOW");
     return e ? std::atoi(e) : 512;  // 2 blocks / CU (measured +1.8 % over 256)
   }();
-  if (cw.phases == 1 && blocks < split_below && nkt * bk >= 512) {
+  if (!pp && cw.phases == 1 && blocks < split_below && nkt * bk >= 512) {
     splits = std::min(std::min(8, std::max(2, 512 / blocks)), nkt * bk / 256);
     ksplit = cdiv(nkt, splits);
     splits = cdiv(nkt, ksplit);
@@ -742,6 +753,23 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
     const int rb = cdiv(M * (cw.cout / 4), 256);
     R.begin("splitk_reduce_kernel", 0.0, 4.0 * (double)(splits + 1) * M * cw.cout);
     splitk_reduce_kernel<<<rb, 256, 0, R.st>>>(q);
+    R.end();
+    HIPCHK(hipGetLastError());
+    return rrows;
+  }
+  if (pp) {  // 512-thread ping-pong kernel, 256 x bn tiles (igemm_pp.h)
+    dim3 gpp(cdiv(M, 256), cdiv(cw.cout, bn), 1);
+    std::snprintf(nm, sizeof nm, "igemm_pp_kernel<%d, %d, %d, %d>", bn, (int)EPI_STATS, x3_sa, x1 ? 1 : 0);
+    R.begin(nm, flops, bytes);
+#define PPK(BNN, SAA, XX) igemm_pp_kernel<BNN, EPI_STATS, SAA, XX><<<gpp, 512, 0, R.st>>>(xp)
+    if (bn == 128) {
+      if (x3_sa) { if (x1) PPK(128, 1, 1); else PPK(128, 1, 0); }
+      else { if (x1) PPK(128, 0, 1); else PPK(128, 0, 0); }
+    } else {
+      if (x3_sa) { if (x1) PPK(64, 1, 1); else PPK(64, 1, 0); }
+      else { if (x1) PPK(64, 0, 1); else PPK(64, 0, 0); }
+    }
+#undef PPK
     R.end();
     HIPCHK(hipGetLastError());
     return rrows;

@@ -43,7 +43,7 @@ struct TokParams {
   int M;
 };
 
-enum { ROWS_SPLIT = 0, ROWS_LN = 1, ROWS_STATS = 2 };
+enum { ROWS_SPLIT = 0, ROWS_LN = 1, ROWS_STATS = 2, ROWS_LNF = 3 };
 
 // DPP lane exchange (no LDS round trip): quad_perm / row_half_mirror / row_mirror.
 template <int CTRL>
@@ -68,7 +68,8 @@ DMX_DEV float group_sum(float s) {
 // same per-element expression as layernorm_kernel.
 template <int C, int TM, int MODE, int NW = 4>
 DMX_DEV void tok_rows(const float* src, int ld, int m0, int M, const float* g, const float* b,
-                      _Float16 (*Ah)[C + 8], _Float16 (*Al)[C + 8], float* mu, float* rs) {
+                      _Float16 (*Ah)[C + 8], _Float16 (*Al)[C + 8], float* mu, float* rs, float* o32 = nullptr,
+                      int ldo = 0) {
   constexpr int G = C / 16, RP = 64 / G, RW = TM / NW, NP = RW / RP;
   static_assert(G == 4 || G == 8 || G == 16, "C");
   static_assert(NP >= 1 && RW % RP == 0, "rows per wave");
@@ -114,6 +115,16 @@ DMX_DEV void tok_rows(const float* src, int ld, int m0, int M, const float* g, c
         if (lane % G == 0) {
           mu[row] = mean;
           rs[row] = rstd;
+        }
+      } else if constexpr (MODE == ROWS_LNF) {  // LN'd rows kept fp32 in LDS (o32[row][c], stride ldo)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int c = c0 + 4 * G * j;
+          const floatx4 gw = ld4(g + c), bw = ld4(b + c);
+          floatx4 y;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) y[e] = (v[p][j][e] - mean) * rstd * gw[e] + bw[e];
+          *reinterpret_cast<floatx4*>(o32 + row * ldo + c) = y;
         }
       } else {
 #pragma unroll
@@ -219,27 +230,28 @@ __global__ __launch_bounds__(NW * 64) void tok_attn_out_kernel(const TokParams P
   __shared__ __attribute__((aligned(16))) _Float16 Ah[TM][C + 8];
   __shared__ __attribute__((aligned(16))) _Float16 Al[TM][C + 8];
   __shared__ __attribute__((aligned(16))) float Av[TM][VS];
-  __shared__ float mu1[TM], rs1[TM];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, fr = lane & 31, fh = lane >> 5;
   const int wm = wid / WC, wn = wid % WC, m0 = blockIdx.x * TM;
   const int M = P.M, nw = wn * CW, arow0 = wm * 32;
 
+  // ao -> A planes; LN1(x) -> Av (fp32, the residual of the out-projection): both loads in flight
+  // together, no second read of x later
   tok_rows<C, TM, ROWS_SPLIT, NW>(P.ao, C, m0, M, nullptr, nullptr, Ah, Al, nullptr, nullptr);
-  tok_rows<C, TM, ROWS_STATS, NW>(P.x, C, m0, M, nullptr, nullptr, Ah, Al, mu1, rs1);
+  tok_rows<C, TM, ROWS_LNF, NW>(P.x, C, m0, M, P.l1w, P.l1b, Ah, Al, nullptr, nullptr, &Av[0][0], VS);
   __syncthreads();
 
   floatx16 acc[NT];
-  // av = ao Wo^T + bo + LN1(x)   (models/unet_cond.py:49-50)
+  // av = ao Wo^T + bo + LN1(x)   (models/unet_cond.py:49-50); each Av element is read and
+  // rewritten by the same lane
   tok_gemm<C, NT, X1>(Ah, Al, P.w0, nw, acc, arow0, fr, fh);
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     const int col = nw + 32 * j + fr;
-    const float bo = P.w0.bias[col], g1 = P.l1w[col], b1 = P.l1b[col];
+    const float bo = P.w0.bias[col];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int row = arow0 + tok_r(fh, r), m = min(m0 + row, M - 1);
-      const float xl = (P.x[(size_t)m * C + col] - mu1[row]) * rs1[row] * g1 + b1;
-      Av[row][col] = (acc[j][r] * P.w0.inv_scale + bo) + xl;
+      const int row = arow0 + tok_r(fh, r);
+      Av[row][col] = (acc[j][r] * P.w0.inv_scale + bo) + Av[row][col];
     }
   }
   __syncthreads();
