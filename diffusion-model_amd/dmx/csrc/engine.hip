@@ -654,9 +654,26 @@ static void launch_x3_tiles(int bm, int bn, const X3Params& p, dim3 grid, hipStr
 // Sources are plain NHWC (or the NCHW network input); grids too small to fill the
 // 256 CUs are split along K into deterministic slabs reduced by splitk_reduce_kernel.
 // Returns the GroupNorm partial rows per sample it wrote (EPI_STATS).
+// `defer` (EPI_STATS only): when the GEMM splits K and one sample fits reduce_norm_kernel,
+// the reduce launch is skipped and the slab handed back (defer->fused) for the caller's
+// fused split-K reduce + GroupNorm.
+struct Deferred {
+  bool fused = false;
+  float* partial = nullptr;
+  int splits = 0;
+  const float* bias = nullptr;
+};
+static bool reduce_norm_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("DMX_REDUCE_NORM");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, const ConvW& cw, int epi, float* out,
                 const float* res, float2* rowpart, int seg, const _Float16* ash = nullptr,
-                const _Float16* asl = nullptr) {
+                const _Float16* asl = nullptr, Deferred* defer = nullptr) {
   const int M = N * H * W;
   if (cw.cout % 32 != 0) throw Error(DMX_E_INTERNAL, "gemm: Cout must be a multiple of 32");
   const int bn = (cw.cout % 128 == 0) ? 128 : 64;
@@ -691,6 +708,13 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   float* partial = splits > 1 ? R.ws.get<float>((size_t)splits * M * cw.cout) : nullptr;
   const int rgrp = (splits == 1 && (H * W) % 32 == 0) ? 32 : 1;
   const int rrows = cw.phases * H * W / rgrp;
+  if (defer != nullptr) {
+    defer->fused = splits > 1 && epi == EPI_STATS && reduce_norm_enabled() && !R.m->debug &&
+                   H * W * (cw.cout / 4) <= RN_MAXV * 1024;  // (debug taps read the raw conv output)
+    defer->partial = partial;
+    defer->splits = splits;
+    defer->bias = cw.bias;
+  }
   if (R.plan) return rrows;
   IgemmParams p;
   std::memset(&p, 0, sizeof(p));
@@ -749,6 +773,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
     else launch_ig_tiles<SRC_PLAIN, EPI_PARTIAL>(bm, bn, p, grid, R.st);
     R.end();
     HIPCHK(hipGetLastError());
+    if (defer != nullptr && defer->fused) return rrows;  // the caller's reduce_norm_kernel sums the slabs
     SplitkParams q{partial, splits, M, cw.cout, cw.bias, res, out, rowpart, seg, epi};
     const int rb = cdiv(M * (cw.cout / 4), 256);
     R.begin("splitk_reduce_kernel", 0.0, 4.0 * (double)(splits + 1) * M * cw.cout);
@@ -833,6 +858,19 @@ static void norm(Run& R, NormParams np, int N) {
   HIPCHK(hipGetLastError());
 }
 
+// Split-K slabs of a deferred GEMM -> GroupNorm(1, C) application (reduce_norm_kernel): one
+// block per source sample; np describes the normalisation exactly as for norm().
+static void reduce_norm(Run& R, const Deferred& d, NormParams np, int n_src_samples) {
+  if (R.plan) return;
+  const int n_out = np.n_src > 0 ? 2 * n_src_samples : n_src_samples;
+  R.begin("reduce_norm_kernel", 0.0,
+          4.0 * (double)n_src_samples * np.HW * np.C * (d.splits + (np.res ? 1 : 0)) +
+              4.0 * (double)n_out * np.HW * np.C * (np.out_h ? 1 : 1));
+  reduce_norm_kernel<<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
+  R.end();
+  HIPCHK(hipGetLastError());
+}
+
 template <int SRC>
 static void prep(Run& R, const SrcDesc& s, float* out, int N, int H, int W, const char* name) {
   if (R.plan) return;
@@ -888,7 +926,8 @@ static float* resblock(Run& R, const ResW& w, const SrcDesc& in, int mode, int N
   float* r2 = R.ws.get<float>((size_t)M * w.cout);
   float2* rp2 = R.ws.get<float2>((size_t)M * (w.cout / seg));
   float* out = R.ws.get<float>((size_t)n_out * HW * w.cout);
-  const int rr1 = gemm(R, in, mode, N, H, W, w.c1, EPI_STATS, r1, nullptr, rp1, seg);
+  Deferred d1, d2;  // split-K convs at low resolution: reduce + GroupNorm in one launch
+  const int rr1 = gemm(R, in, mode, N, H, W, w.c1, EPI_STATS, r1, nullptr, rp1, seg, nullptr, nullptr, &d1);
   NormParams n1 = norm_params(r1, rp1, w.mid / seg, rr1, w.g1.p, w.b1.p, w.mid, HW, a1);
   n1.act = 1;
   _Float16* a1h = reinterpret_cast<_Float16*>(a1);
@@ -898,9 +937,10 @@ static float* resblock(Run& R, const ResW& w, const SrcDesc& in, int mode, int N
     n1.out_h = a1h;
     n1.out_l = a1l;
   }
-  norm(R, n1, N);
+  if (d1.fused) reduce_norm(R, d1, n1, N);
+  else norm(R, n1, N);
   const int rr2 = gemm(R, plain_src(a1, w.mid), SRC_PLAIN, N, H, W, w.c2, EPI_STATS, r2, nullptr, rp2, seg,
-                       planes ? a1h : nullptr, planes ? a1l : nullptr);
+                       planes ? a1h : nullptr, planes ? a1l : nullptr, &d2);
   NormParams n2 = norm_params(r2, rp2, w.cout / seg, rr2, w.g2.p, w.b2.p, w.cout, HW, out);
   if (residual) {
     if (mode != SRC_PLAIN) throw Error(DMX_E_INTERNAL, "residual ResBlock needs a plain input");
@@ -910,7 +950,8 @@ static float* resblock(Run& R, const ResW& w, const SrcDesc& in, int mode, int N
   n2.emb_stride = emb_stride;
   n2.emb_off = emb_off;
   n2.n_src = n_out > N ? N : 0;
-  norm(R, n2, n_out);
+  if (d2.fused) reduce_norm(R, d2, n2, N);
+  else norm(R, n2, n_out);
   R.tap(R.layer + ".r1", r1, (size_t)M * w.mid);
   R.tap(R.layer, out, (size_t)n_out * HW * w.cout);
   return out;

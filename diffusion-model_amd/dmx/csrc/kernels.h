@@ -239,6 +239,108 @@ __global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
   }
 }
 
+// Split-K reduction fused with GroupNorm(1, C) for the small low-resolution convolutions
+// (one 1024-thread block per source sample, the whole sample — HW*C <= RN_MAXV*4096 values —
+// held in registers): sums the split slabs in split order (+ bias), reduces the sample's
+// (sum, sum of squares) in double in a fixed order, then applies exactly norm_kernel's
+// GroupNorm (+GELU | +residual GELU) (+emb) and writes fp32 and / or f16 hi/lo planes,
+// including the CFG fan-out (n_src > 0: outputs s and s + n_src both come from source s).
+// Replaces splitk_reduce_kernel + norm_kernel (two launches, two HBM round trips of the
+// conv output) at 8x8 / 4x4 where both are launch-latency bound.
+constexpr int RN_MAXV = 8;  // float4 per thread
+
+__global__ __launch_bounds__(1024) void reduce_norm_kernel(const float* partial, int splits, const float* bias,
+                                                           const NormParams p) {
+  const int s = blockIdx.x, tid = threadIdx.x;
+  const int C4 = p.C >> 2, per = p.HW * C4;
+  const size_t sstride = (size_t)gridDim.x * per * 4;  // floats per split slab (all source samples)
+  const size_t sbase = (size_t)s * per * 4;
+  floatx4 v[RN_MAXV];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < RN_MAXV; ++k) {
+    const int idx = tid + 1024 * k;
+    v[k] = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (idx < per) {
+      for (int sp = 0; sp < splits; ++sp) {
+        const floatx4 a = ld4(partial + sp * sstride + sbase + (size_t)idx * 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[k][j] += a[j];
+      }
+      if (bias != nullptr) {
+        const floatx4 b = ld4(bias + (idx % C4) * 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[k][j] += b[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s1 += v[k][j];
+        s2 += v[k][j] * v[k][j];
+      }
+    }
+  }
+  __shared__ double r1[16], r2[16];
+  __shared__ float2 st_s;
+  double d1 = s1, d2 = s2;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    d1 += __shfl_xor(d1, o, 64);
+    d2 += __shfl_xor(d2, o, 64);
+  }
+  if ((tid & 63) == 0) {
+    r1[tid >> 6] = d1;
+    r2[tid >> 6] = d2;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double a1 = 0.0, a2 = 0.0;
+    for (int w = 0; w < 16; ++w) {
+      a1 += r1[w];
+      a2 += r2[w];
+    }
+    const double cnt = (double)p.HW * (double)p.C;
+    const double mean = a1 / cnt;
+    double var = a2 / cnt - mean * mean;
+    var = var < 0.0 ? 0.0 : var;
+    st_s = make_float2((float)mean, (float)(1.0 / sqrt(var + 1e-5)));
+  }
+  __syncthreads();
+  const float2 st = st_s;
+  const int nout = p.n_src > 0 ? 2 : 1;
+  for (int q = 0; q < nout; ++q) {
+    const int n = s + q * (p.n_src > 0 ? p.n_src : 0);
+    const size_t base = (size_t)n * per * 4;
+#pragma unroll
+    for (int k = 0; k < RN_MAXV; ++k) {
+      const int idx = tid + 1024 * k;
+      if (idx >= per) break;
+      const int c = (idx % C4) * 4;
+      floatx4 o = gn_apply4(v[k], st, p.gamma, p.beta, c, 0);
+      if (p.res != nullptr) {
+        const floatx4 r = ld4(p.res + sbase + (size_t)idx * 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = gelu(r[j] + o[j]);
+      } else if (p.act) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = gelu(o[j]);
+      }
+      if (p.emb != nullptr) {
+        const floatx4 e = ld4(p.emb + (size_t)n * p.emb_stride + p.emb_off + c);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] += e[j];
+      }
+      const size_t off = base + (size_t)idx * 4;
+      if (p.out != nullptr) *reinterpret_cast<floatx4*>(p.out + off) = o;
+      if (p.out_h != nullptr) {
+        half4 hh, ll;
+        split4(o, hh, ll);
+        *reinterpret_cast<half4*>(p.out_h + off) = hh;
+        *reinterpret_cast<half4*>(p.out_l + off) = ll;
+      }
+    }
+  }
+}
+
 // Materialise a fused source (2x2 max-pool, bilinear-x2 + pad + concat) as a plain
 // NHWC tensor [N][H][W][C] (models/unet_cond.py:58, 88-97).
 template <int SRC>
