@@ -677,8 +677,12 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   const int M = N * H * W;
   if (cw.cout % 32 != 0) throw Error(DMX_E_INTERNAL, "gemm: Cout must be a multiple of 32");
   const int bn = (cw.cout % 128 == 0) ? 128 : 64;
+  static const int bm128_min = [] {  // 128-row tiles (split K if the grid is then small) from this many tiles
+    const char* e = std::getenv("DMX_BM128_MIN");
+    return e ? std::atoi(e) : 256;  // measured +0.6 % over 512 (8x8x512 and 32x32x128 layers split in 2)
+  }();
   const int tiles128 = cdiv(M, 128) * cdiv(cw.cout, bn) * cw.phases;
-  const int bm = tiles128 >= 512 ? 128 : 64;
+  const int bm = tiles128 >= bm128_min ? 128 : 64;
   const int blocks = cdiv(M, bm) * cdiv(cw.cout, bn) * cw.phases;
   const bool x3 = R.m->prec >= 1 && src_mode == SRC_PLAIN && cw.Bh != nullptr;
   const bool x1 = x3 && R.m->prec == 2;  // config-4 fp16: one MFMA on the hi planes
@@ -753,6 +757,14 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   xp.Bh = cw.Bh;
   xp.Bl = cw.Bl;
   xp.inv_scale = cw.inv_scale;
+  {
+    const size_t a_el = (size_t)N * p.Hin * p.Win * s.C;
+    const size_t ab = a_el * (ash != nullptr ? 2 : 4), bb = (size_t)cw.npad * cw.kpad * 2;
+    if (x3 && (ab >= ((size_t)1 << 31) || bb >= ((size_t)1 << 31)))
+      throw Error(DMX_E_ARG, "gemm: operand too large for 32-bit buffer offsets (split the batch)");
+    xp.a_bytes = (unsigned)ab;
+    xp.b_bytes = (unsigned)bb;
+  }
   // labels are the demangled kernel names rocprofv3 reports (profiles/ cross-check)
   const char* kname = x3 ? "igemm_x3_kernel" : "igemm_f32_kernel";
   const int x3_nbuf = (x1 || x3_pipe() == 1 || x3_pipe() == 2) ? 1 : 2, x3_sa = ash != nullptr ? 1 : 0;

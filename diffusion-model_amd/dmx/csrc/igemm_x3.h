@@ -32,10 +32,25 @@ struct X3Params {
   const _Float16* Bh;      // [phases][Npad][Kpad] scaled hi
   const _Float16* Bl;      //                      scaled lo
   float inv_scale;         // 2^-e
+  unsigned a_bytes;        // bytes of the A source (one plane) — buffer-load range
+  unsigned b_bytes;        // bytes of one phase of one B plane ([Npad][Kpad] f16)
 };
 
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// Buffer-resource loads (32-bit offsets, descriptor in SGPRs): an offset at or past the range
+// returns zeros, which is how padding taps / rows past M are masked.
+constexpr int kOOB = 0x7ffffff0;
+DMX_DEV __amdgpu_buffer_rsrc_t rsrc_of(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+DMX_DEV half8 bload_h8(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+DMX_DEV floatx4 bload_f4(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
 
 // hi/lo split of two fp32 values as packed f16 pairs (common.h split2u: 3 VALU ops per pair).
 DMX_DEV void split2(f32x2 v, unsigned& h, unsigned& l) { split2u(v.x, v.y, h, l); }
@@ -97,6 +112,18 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
     lc = k - ltap * C;
   };
   const float* __restrict__ asrc = p.src.src0;
+#ifndef DMX_NO_BUFLOAD
+  // Buffer-resource addressing: 32-bit byte offsets; a masked piece gets an out-of-range offset
+  // and reads zeros (no 64-bit address math / selects per piece); B offsets are per-thread
+  // constants plus a wave-uniform K-tile offset.
+  constexpr int AES = SPLIT_A ? 2 : 4;  // bytes per A element
+  const __amdgpu_buffer_rsrc_t rAh = rsrc_of(SPLIT_A ? (const void*)P.Ash : (const void*)asrc, P.a_bytes);
+  const __amdgpu_buffer_rsrc_t rAl = rsrc_of(SPLIT_A ? (const void*)P.Asl : (const void*)asrc, P.a_bytes);
+  const __amdgpu_buffer_rsrc_t rBh = rsrc_of(Bh, P.b_bytes), rBl = rsrc_of(Bl, P.b_bytes);
+  int boffs[BP];
+#pragma unroll
+  for (int i = 0; i < BP; ++i) boffs[i] = ((n0 + rb + i * BRS) * p.Kpad + qb * 8) * 2;
+#endif
   auto load_tile = [&](int kt) {
     int ddy, ddx;
     tap_offset(p.geom, phase, ltap, ddy, ddx);
@@ -109,11 +136,20 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
     }
 #pragma unroll
     for (int i = 0; i < AP; ++i) {
-      // Padding taps / rows past M read 16 zero bytes from g_zero16: the select is on the
-      // ADDRESS, so nothing consumes the loaded data before store_tile and the loads stay
-      // in flight across compute() (a select on the data forced a vmcnt wait before the MFMAs).
+      // Padding taps / rows past M read zeros: the select is on the ADDRESS, so nothing
+      // consumes the loaded data before store_tile and the loads stay in flight across
+      // compute() (a select on the data forced a vmcnt wait before the MFMAs).
       const bool ok = (tmask[i] >> tap) & 1u;
       const int off = (rpix[i] + delta) * C + c;
+#ifndef DMX_NO_BUFLOAD
+      const int boff_a = ok ? off * AES : kOOB;
+      if constexpr (SPLIT_A) {
+        rah[i] = bload_h8(rAh, boff_a, 0);
+        if constexpr (!X1) ral[i] = bload_h8(rAl, boff_a, 0);
+      } else {
+        ra4[i] = bload_f4(rAh, boff_a, 0);
+      }
+#else
       if constexpr (SPLIT_A) {
         const _Float16* ph = ok ? P.Ash + off : reinterpret_cast<const _Float16*>(g_zero16);
         rah[i] = *reinterpret_cast<const half8*>(ph);
@@ -124,12 +160,18 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
       } else {
         ra4[i] = ld4(ok ? asrc + off : g_zero16);
       }
+#endif
     }
 #pragma unroll
     for (int i = 0; i < BP; ++i) {
+#ifndef DMX_NO_BUFLOAD
+      rbh[i] = bload_h8(rBh, boffs[i], kt * BK * 2);
+      if constexpr (!X1) rbl[i] = bload_h8(rBl, boffs[i], kt * BK * 2);
+#else
       const size_t o = (size_t)(n0 + rb + i * BRS) * p.Kpad + kt * BK + qb * 8;
       rbh[i] = *reinterpret_cast<const half8*>(Bh + o);
       if constexpr (!X1) rbl[i] = *reinterpret_cast<const half8*>(Bl + o);
+#endif
     }
   };
   auto store_tile = [&](int buf) {
