@@ -88,6 +88,12 @@ __global__ __launch_bounds__(512) void igemm_pp_kernel(const X3Params P) {
     lc = k - ltap * C;
   };
   const float* __restrict__ asrc = p.src.src0;
+  // buffer-resource addressing as in igemm_x3_kernel (out-of-range offset = zero padding)
+  constexpr int AES = SPLIT_A ? 2 : 4;
+  const __amdgpu_buffer_rsrc_t rAh = rsrc_of(SPLIT_A ? (const void*)P.Ash : (const void*)asrc, P.a_bytes);
+  const __amdgpu_buffer_rsrc_t rAl = rsrc_of(SPLIT_A ? (const void*)P.Asl : (const void*)asrc, P.a_bytes);
+  const __amdgpu_buffer_rsrc_t rBh = rsrc_of(Bh, P.b_bytes), rBl = rsrc_of(Bl, P.b_bytes);
+  const int boffs = ((n0 + rb) * p.Kpad + qb * 8) * 2;
   // K-tiles must be loaded in order (incremental tap / channel tracking)
   auto load_tile = [&](int kt, Stage& st) {
     int ddy, ddx;
@@ -101,23 +107,18 @@ __global__ __launch_bounds__(512) void igemm_pp_kernel(const X3Params P) {
     }
 #pragma unroll
     for (int i = 0; i < AP; ++i) {
-      const bool ok = (tmask[i] >> tap) & 1u;  // padding taps / rows past M read the zero page
-      const int off = (rpix[i] + delta) * C + c;
+      const bool ok = (tmask[i] >> tap) & 1u;  // padding taps / rows past M read zeros
+      const int boff_a = ok ? ((rpix[i] + delta) * C + c) * AES : kOOB;
       if constexpr (SPLIT_A) {
-        const _Float16* ph = ok ? P.Ash + off : reinterpret_cast<const _Float16*>(g_zero16);
-        st.rah[i] = *reinterpret_cast<const half8*>(ph);
-        if constexpr (!X1) {
-          const _Float16* pl = ok ? P.Asl + off : reinterpret_cast<const _Float16*>(g_zero16);
-          st.ral[i] = *reinterpret_cast<const half8*>(pl);
-        }
+        st.rah[i] = bload_h8(rAh, boff_a, 0);
+        if constexpr (!X1) st.ral[i] = bload_h8(rAl, boff_a, 0);
       } else {
-        st.ra4[i] = ld4(ok ? asrc + off : g_zero16);
+        st.ra4[i] = bload_f4(rAh, boff_a, 0);
       }
     }
     if (bact) {
-      const size_t o = (size_t)(n0 + rb) * p.Kpad + kt * BK + qb * 8;
-      st.rbh = *reinterpret_cast<const half8*>(Bh + o);
-      if constexpr (!X1) st.rbl = *reinterpret_cast<const half8*>(Bl + o);
+      st.rbh = bload_h8(rBh, boffs, kt * BK * 2);
+      if constexpr (!X1) st.rbl = bload_h8(rBl, boffs, kt * BK * 2);
     }
   };
   auto store_tile = [&](int buf, const Stage& st) {
