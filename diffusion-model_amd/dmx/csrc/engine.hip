@@ -1046,9 +1046,36 @@ static float* attn_block_fused(Run& R, const AttnW& a, const float* x, int N, in
       const char* e = std::getenv("DMX_TOK_NB256");
       return e ? std::atoi(e) : 64;
     }();
+    static const bool lds_w = [] {  // weight slice resident in LDS, several token tiles per block
+      const char* e = std::getenv("DMX_TOK_LDS");
+      return e ? std::atoi(e) != 0 : true;
+    }();
+    const int x1 = R.m->prec == 2 ? 1 : 0;
+    if (lds_w && (C == 64 || C == 128)) {
+      const int nbl = C == 64 ? 192 : 64, gy = 3 * C / nbl, tiles = cdiv(M, 64);
+      const int tpb = cdiv(tiles, 4) * gy >= 512 ? 4 : cdiv(tiles, 2) * gy >= 512 ? 2 : 1;
+      const dim3 gl(cdiv(tiles, tpb), gy);
+      R.begin("tok_ln_qkv_lds_kernel<" + cs + ", " + std::to_string(nbl) + ", " + std::to_string(tpb) + ", " +
+                  std::to_string(x1) + ">",
+              2.0 * M * C * 3.0 * C, 16.0 * (double)M * C);
+#define TQL(CC, NN, TT) (x1 ? tok_ln_qkv_lds_kernel<CC, NN, TT, 1><<<gl, 256, 0, R.st>>>(tp) \
+                            : tok_ln_qkv_lds_kernel<CC, NN, TT, 0><<<gl, 256, 0, R.st>>>(tp))
+      if (C == 64) {
+        if (tpb == 4) TQL(64, 192, 4);
+        else if (tpb == 2) TQL(64, 192, 2);
+        else TQL(64, 192, 1);
+      } else {
+        if (tpb == 4) TQL(128, 64, 4);
+        else if (tpb == 2) TQL(128, 64, 2);
+        else TQL(128, 64, 1);
+      }
+#undef TQL
+      R.end();
+      HIPCHK(hipGetLastError());
+    }
     const int nb = C == 64 ? nb64 : C == 256 ? nb256 : 128;  // output columns per block (grid.y = 3C / nb)
     const dim3 grid(cdiv(M, 64), 3 * C / nb);
-    const int x1 = R.m->prec == 2 ? 1 : 0;
+    if (!(lds_w && (C == 64 || C == 128))) {
     R.begin("tok_ln_qkv_kernel<" + cs + ", " + std::to_string(nb) + ", " + std::to_string(x1) + ">",
             2.0 * M * C * 3.0 * C, 16.0 * (double)M * C);
 #define TQ(CC, NN) (x1 ? tok_ln_qkv_kernel<CC, NN, 1><<<grid, 256, 0, R.st>>>(tp) \
@@ -1067,6 +1094,7 @@ static float* attn_block_fused(Run& R, const AttnW& a, const float* x, int N, in
 #undef TQ
     R.end();
     HIPCHK(hipGetLastError());
+    }
   }
   attention_core(R, qkv, ao, N, L, C);
   if (!R.plan) {

@@ -221,6 +221,79 @@ __global__ __launch_bounds__(256) void tok_ln_qkv_kernel(const TokParams P) {
   }
 }
 
+// acc[j] = A[arow0 .. +32][0, C) . W[nw + 32j .. +32][0, C)^T with W staged in LDS planes
+// ([rows][C + 8], the A planes' conflict-free stride).
+template <int C, int NT, int X1 = 0>
+DMX_DEV void tok_gemm_lds(const _Float16 (*Ah)[C + 8], const _Float16 (*Al)[C + 8], const _Float16 (*Wh)[C + 8],
+                          const _Float16 (*Wl)[C + 8], int nw, floatx16 (&acc)[NT], int arow0, int fr, int fh) {
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  const int arow = arow0 + fr;
+#pragma unroll
+  for (int s = 0; s < C / 16; ++s) {
+    const half8 ah = *reinterpret_cast<const half8*>(&Ah[arow][16 * s + 8 * fh]);
+    half8 al;
+    if constexpr (!X1) al = *reinterpret_cast<const half8*>(&Al[arow][16 * s + 8 * fh]);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const half8 bh = *reinterpret_cast<const half8*>(&Wh[nw + 32 * j + fr][16 * s + 8 * fh]);
+      if constexpr (!X1) {
+        const half8 bl = *reinterpret_cast<const half8*>(&Wl[nw + 32 * j + fr][16 * s + 8 * fh]);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[j], 0, 0, 0);
+      }
+      acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[j], 0, 0, 0);
+    }
+  }
+}
+
+// TA with the weight slice resident in LDS: the block stages rows [blockIdx.y * NB, +NB) of
+// the in_proj hi / lo planes once, then runs TPB consecutive 64-token tiles (LN1 -> planes ->
+// GEMM -> store).  Per 64 tokens the B-fragment reads of tok_ln_qkv_kernel (NB x C x 4 bytes
+// from L2, 3x the activation bytes at C = 64) become LDS reads.
+template <int C, int NB, int TPB, int X1 = 0>
+__global__ __launch_bounds__(256) void tok_ln_qkv_lds_kernel(const TokParams P) {
+  constexpr int NT = NB / 64;
+  __shared__ __attribute__((aligned(16))) _Float16 Wh[NB][C + 8];
+  __shared__ __attribute__((aligned(16))) _Float16 Wl[X1 ? 1 : NB][C + 8];
+  __shared__ __attribute__((aligned(16))) _Float16 Ah[64][C + 8];
+  __shared__ __attribute__((aligned(16))) _Float16 Al[64][C + 8];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, fr = lane & 31, fh = lane >> 5;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int nb0 = blockIdx.y * NB;
+  constexpr int CPR = C / 8;  // 16-byte chunks per weight row
+  for (int i = tid; i < NB * CPR; i += 256) {
+    const int r = i / CPR, q = i % CPR;
+    const size_t o = (size_t)(nb0 + r) * P.w0.kpad + q * 8;
+    *reinterpret_cast<half8*>(&Wh[r][q * 8]) = *reinterpret_cast<const half8*>(P.w0.h + o);
+    if constexpr (!X1) *reinterpret_cast<half8*>(&Wl[r][q * 8]) = *reinterpret_cast<const half8*>(P.w0.l + o);
+  }
+  const int nwl = wn * (NB / 2);  // this wave's first column inside the slice
+  float bias[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) bias[j] = P.w0.bias[nb0 + nwl + 32 * j + fr];
+  for (int t = 0; t < TPB; ++t) {
+    const int m0 = (blockIdx.x * TPB + t) * 64;
+    if (m0 >= P.M) break;
+    tok_rows<C, 64, ROWS_LN>(P.x, C, m0, P.M, P.l1w, P.l1b, Ah, Al, nullptr, nullptr);
+    __syncthreads();
+    floatx16 acc[NT];
+    tok_gemm_lds<C, NT, X1>(Ah, Al, Wh, Wl, nwl, acc, wm * 32, fr, fh);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int col = nb0 + nwl + 32 * j + fr;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 32 + tok_r(fh, r);
+        if (m < P.M) P.out[(size_t)m * 3 * C + col] = acc[j][r] * P.w0.inv_scale + bias[j];
+      }
+    }
+    __syncthreads();  // every wave is done with this tile's planes
+  }
+}
+
 // TB: out-proj + residual, LN2, FF1 + GELU, FF2 + residual for TM tokens x all C channels.
 // NW waves: TM = 64: 2 (rows) x NW/2 (cols); TM = 32: 1 x NW (more blocks for small M / wide C).
 template <int C, int TM, int X1 = 0, int NW = 4>
