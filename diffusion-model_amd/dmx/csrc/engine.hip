@@ -1365,10 +1365,16 @@ static void step_body(Run& R, const dmx_step_args& a) {
   p.noise = a.noise;
   p.seed = a.seed;
   p.sample_offset = a.sample_offset;
-  dim3 grid(cdiv(p.HW, 256), a.n);
   R.layer = "out+cfg+ddpm";
-  R.begin("step_tail_kernel", 2.0 * N * p.HW * 64.0 * p.Co, 4.0 * ((double)N * p.HW * 64 + 3.0 * a.n * p.HW * p.Co));
-  step_tail_kernel<<<grid, 256, 0, R.st>>>(p);
+  if (p.Co == 4 && p.feat != nullptr) {
+    dim3 grid(cdiv(p.HW, 16), a.n);
+    R.begin("step_tail4_kernel", 2.0 * N * p.HW * 64.0 * p.Co, 4.0 * ((double)N * p.HW * 64 + 3.0 * a.n * p.HW * p.Co));
+    step_tail4_kernel<<<grid, 256, 0, R.st>>>(p);
+  } else {
+    dim3 grid(cdiv(p.HW, 256), a.n);
+    R.begin("step_tail_kernel", 2.0 * N * p.HW * 64.0 * p.Co, 4.0 * ((double)N * p.HW * 64 + 3.0 * a.n * p.HW * p.Co));
+    step_tail_kernel<<<grid, 256, 0, R.st>>>(p);
+  }
   R.end();
   HIPCHK(hipGetLastError());
 }
