@@ -65,13 +65,20 @@ __global__ __launch_bounds__(256) void embed_kernel(const EmbedParams p) {
     for (int j = 0; j < 24; ++j) a += p.w0[k * 24 + j] * in24[j];
     h[k] = silu(a);
     __syncthreads();
+    // 32 independent L2 loads in flight per wait (the weights are L2-resident; with 4 the
+    // two 256-long dot products were a chain of 128 L2 round trips)
     float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
-#pragma unroll 4
-    for (int j = 0; j < 256; j += 4) {
-      c0 += p.w2t[(j + 0) * 256 + k] * h[j + 0];
-      c1 += p.w2t[(j + 1) * 256 + k] * h[j + 1];
-      c2 += p.w2t[(j + 2) * 256 + k] * h[j + 2];
-      c3 += p.w2t[(j + 3) * 256 + k] * h[j + 3];
+    for (int j0 = 0; j0 < 256; j0 += 32) {
+      float wv[32];
+#pragma unroll
+      for (int u = 0; u < 32; ++u) wv[u] = p.w2t[(j0 + u) * 256 + k];
+#pragma unroll
+      for (int u = 0; u < 32; u += 4) {
+        c0 += wv[u + 0] * h[j0 + u + 0];
+        c1 += wv[u + 1] * h[j0 + u + 1];
+        c2 += wv[u + 2] * h[j0 + u + 2];
+        c3 += wv[u + 3] * h[j0 + u + 3];
+      }
     }
     v += p.b2[k] + ((c0 + c1) + (c2 + c3));
   }
@@ -635,6 +642,63 @@ __global__ __launch_bounds__(256) void step_tail_kernel(const StepTailParams p) 
     const size_t idx = ((size_t)n * Co + c) * p.HW + pix;
     p.x_out[idx] = ddpm_elem(p.x[idx], eps, c1, c2, sd, nz[c]);
   }
+}
+
+// step_tail_kernel for the network head path (feat given, Co = 4): 16 lanes per pixel, each
+// loading one float4 of the pixel's 64 features (a wave reads 4 whole 256-byte rows, fully
+// coalesced, instead of 64 rows at a 256-byte lane stride); the 1x1-conv dot products are
+// reduced over the 16 lanes with DPP (fixed order), then lanes 0..3 of the group finish
+// channel c = lane (CFG mix, posterior mean, Philox noise, store).
+DMX_DEV float group_sum16(float s) {  // sum over aligned 16-lane rows (DPP), same bits in every lane
+  auto dpp = [](float v, auto ctrl) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), decltype(ctrl)::value,
+                                                                 0xF, 0xF, false));
+  };
+  s += dpp(s, std::integral_constant<int, 0xB1>{});   // quad_perm [1,0,3,2]
+  s += dpp(s, std::integral_constant<int, 0x4E>{});   // quad_perm [2,3,0,1]
+  s += dpp(s, std::integral_constant<int, 0x141>{});  // row_half_mirror
+  s += dpp(s, std::integral_constant<int, 0x140>{});  // row_mirror
+  return s;
+}
+
+__global__ __launch_bounds__(256) void step_tail4_kernel(const StepTailParams p) {
+  const int sub = threadIdx.x & 15, pix = blockIdx.x * 16 + (threadIdx.x >> 4), n = blockIdx.y;
+  const bool valid = pix < p.HW;
+  const int pc = valid ? pix : 0;
+  const floatx4 a = ld4(p.feat + ((size_t)n * p.HW + pc) * 64 + 4 * sub);
+  floatx4 bb = {0.f, 0.f, 0.f, 0.f};
+  if (p.cfg) bb = ld4(p.feat + ((size_t)(n + p.B) * p.HW + pc) * 64 + 4 * sub);
+  float eu[4], ec[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const floatx4 w = ld4(p.w + c * 64 + 4 * sub);
+    float su = 0.f, sc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      su += w[j] * a[j];
+      sc += w[j] * bb[j];
+    }
+    eu[c] = p.b[c] + group_sum16(su);
+    ec[c] = p.b[c] + group_sum16(sc);
+  }
+  if (!valid || sub >= 4) return;
+  int64_t t = p.t[(size_t)n * p.t_stride];
+  t = t < 1 ? 1 : (t > p.tmax ? p.tmax : t);
+  const int c = sub;
+  const float u = sub == 0 ? eu[0] : sub == 1 ? eu[1] : sub == 2 ? eu[2] : eu[3];
+  const float v = sub == 0 ? ec[0] : sub == 1 ? ec[1] : sub == 2 ? ec[2] : ec[3];
+  float nz = 0.f;
+  const size_t idx = ((size_t)n * 4 + c) * p.HW + pix;
+  if (t != 1) {
+    if (p.noise != nullptr) {
+      nz = p.noise[idx];
+    } else {
+      const floatx4 r = normal4(p.seed, (uint64_t)t, ((uint64_t)(n + p.sample_offset) * p.HW + pix));
+      nz = c == 0 ? r[0] : c == 1 ? r[1] : c == 2 ? r[2] : r[3];
+    }
+  }
+  const float eps = p.cfg ? u + rnd(p.guidance * rnd(v - u)) : u;
+  p.x_out[idx] = ddpm_elem(p.x[idx], eps, p.c1[t - 1], p.c2[t - 1], p.sd[t - 1], nz);
 }
 
 // conv1x1 64 -> Co + bias into NCHW (models/unet_cond.py:153, the `out` layer).
