@@ -65,20 +65,13 @@ __global__ __launch_bounds__(256) void embed_kernel(const EmbedParams p) {
     for (int j = 0; j < 24; ++j) a += p.w0[k * 24 + j] * in24[j];
     h[k] = silu(a);
     __syncthreads();
-    // 32 independent L2 loads in flight per wait (the weights are L2-resident; with 4 the
-    // two 256-long dot products were a chain of 128 L2 round trips)
     float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
-    for (int j0 = 0; j0 < 256; j0 += 32) {
-      float wv[32];
-#pragma unroll
-      for (int u = 0; u < 32; ++u) wv[u] = p.w2t[(j0 + u) * 256 + k];
-#pragma unroll
-      for (int u = 0; u < 32; u += 4) {
-        c0 += wv[u + 0] * h[j0 + u + 0];
-        c1 += wv[u + 1] * h[j0 + u + 1];
-        c2 += wv[u + 2] * h[j0 + u + 2];
-        c3 += wv[u + 3] * h[j0 + u + 3];
-      }
+#pragma unroll 4
+    for (int j = 0; j < 256; j += 4) {
+      c0 += p.w2t[(j + 0) * 256 + k] * h[j + 0];
+      c1 += p.w2t[(j + 1) * 256 + k] * h[j + 1];
+      c2 += p.w2t[(j + 2) * 256 + k] * h[j + 2];
+      c3 += p.w2t[(j + 3) * 256 + k] * h[j + 3];
     }
     v += p.b2[k] + ((c0 + c1) + (c2 + c3));
   }
