@@ -258,15 +258,24 @@ __global__ __launch_bounds__(1024) void reduce_norm_kernel(const float* partial,
   floatx4 v[RN_MAXV];
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
+  for (int k = 0; k < RN_MAXV; ++k) v[k] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // split-major: each slab's RN_MAXV loads are issued together (one wait per slab, not per load)
+  for (int sp = 0; sp < splits; ++sp) {
+    floatx4 a[RN_MAXV];
+#pragma unroll
+    for (int k = 0; k < RN_MAXV; ++k) {
+      const int idx = tid + 1024 * k;
+      a[k] = idx < per ? ld4(partial + sp * sstride + sbase + (size_t)idx * 4) : floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int k = 0; k < RN_MAXV; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[k][j] += a[k][j];
+  }
+#pragma unroll
   for (int k = 0; k < RN_MAXV; ++k) {
     const int idx = tid + 1024 * k;
-    v[k] = floatx4{0.f, 0.f, 0.f, 0.f};
     if (idx < per) {
-      for (int sp = 0; sp < splits; ++sp) {
-        const floatx4 a = ld4(partial + sp * sstride + sbase + (size_t)idx * 4);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[k][j] += a[j];
-      }
       if (bias != nullptr) {
         const floatx4 b = ld4(bias + (idx % C4) * 4);
 #pragma unroll
