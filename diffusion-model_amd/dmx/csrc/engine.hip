@@ -1118,14 +1118,29 @@ static float* attn_block_fused(Run& R, const AttnW& a, const float* x, int N, in
       const char* e = std::getenv("DMX_TOK_NW256");
       return e ? std::atoi(e) : 8;
     }();
-    const int nw = C == 256 ? nw256 : 4;
-    R.begin("tok_attn_out_kernel<" + std::to_string(C) + ", " + std::to_string(tm) + ", " + std::to_string(x1) +
-                ", " + std::to_string(nw) + ">",
+    static const bool tb_lds = [] {  // C = 64: weights in LDS, 128-token tiles, 8 waves, several tiles / block
+      const char* e = std::getenv("DMX_TOKB_LDS");
+      return e ? std::atoi(e) != 0 : true;
+    }();
+    const bool lds64 = tb_lds && C == 64;
+    const int tiles128 = cdiv(M, 128), tpb = lds64 ? (tiles128 >= 1024 ? 4 : tiles128 >= 512 ? 2 : 1) : 1;
+    const int nw = C == 256 ? nw256 : lds64 ? 8 : 4;
+    const int tmk = lds64 ? 128 : tm;
+    R.begin("tok_attn_out_kernel<" + std::to_string(C) + ", " + std::to_string(tmk) + ", " + std::to_string(x1) +
+                ", " + std::to_string(nw) + ", " + std::to_string(lds64 ? 1 : 0) + ", " + std::to_string(tpb) + ">",
             6.0 * M * (double)C * C,
             12.0 * (double)M * C);
 #define TB(CC, TT) (x1 ? tok_attn_out_kernel<CC, TT, 1><<<blocks, 256, 0, R.st>>>(tp) \
                        : tok_attn_out_kernel<CC, TT, 0><<<blocks, 256, 0, R.st>>>(tp))
-    if (C == 64) TB(64, 64);
+    if (lds64) {
+      const int bl = cdiv(tiles128, tpb);
+#define TBL(TP) (x1 ? tok_attn_out_kernel<64, 128, 1, 8, 1, TP><<<bl, 512, 0, R.st>>>(tp) \
+                    : tok_attn_out_kernel<64, 128, 0, 8, 1, TP><<<bl, 512, 0, R.st>>>(tp))
+      if (tpb == 4) TBL(4);
+      else if (tpb == 2) TBL(2);
+      else TBL(1);
+#undef TBL
+    } else if (C == 64) TB(64, 64);
     else if (C == 128 && tm == 64) TB(128, 64);
     else if (C == 128) TB(128, 32);
     else if (nw == 8) {

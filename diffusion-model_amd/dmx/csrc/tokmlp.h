@@ -295,70 +295,95 @@ __global__ __launch_bounds__(256) void tok_ln_qkv_lds_kernel(const TokParams P) 
 }
 
 // TB: out-proj + residual, LN2, FF1 + GELU, FF2 + residual for TM tokens x all C channels.
-// NW waves: TM = 64: 2 (rows) x NW/2 (cols); TM = 32: 1 x NW (more blocks for small M / wide C).
-template <int C, int TM, int X1 = 0, int NW = 4>
+// NW waves: TM = 64: 2 (rows) x NW/2 (cols); TM = 32: 1 x NW (more blocks for small M / wide C);
+// TM = 128: 4 x NW/4.  WLDS = 1: the three C x C weights (hi / lo planes) are staged in LDS
+// once per block and the block runs TPB consecutive token tiles (C = 64: the weights are 3x
+// the tile's activation bytes, re-read from L2 per tile otherwise).
+template <int C, int TM, int X1 = 0, int NW = 4, int WLDS = 0, int TPB = 1>
 __global__ __launch_bounds__(NW * 64) void tok_attn_out_kernel(const TokParams P) {
   constexpr int WR = TM / 32, WC = NW / WR, CW = C / WC, NT = CW / 32, VS = C + 4;
   static_assert(NT >= 1, "tile");
+  constexpr int NWS = WLDS ? 3 : 1, WRW = WLDS ? C : 1, WRL = (WLDS && !X1) ? C : 1;
   __shared__ __attribute__((aligned(16))) _Float16 Ah[TM][C + 8];
   __shared__ __attribute__((aligned(16))) _Float16 Al[TM][C + 8];
   __shared__ __attribute__((aligned(16))) float Av[TM][VS];
+  __shared__ __attribute__((aligned(16))) _Float16 Wh[NWS][WRW][C + 8];
+  __shared__ __attribute__((aligned(16))) _Float16 Wl[NWS][WRL][C + 8];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, fr = lane & 31, fh = lane >> 5;
-  const int wm = wid / WC, wn = wid % WC, m0 = blockIdx.x * TM;
+  const int wm = wid / WC, wn = wid % WC;
   const int M = P.M, nw = wn * CW, arow0 = wm * 32;
-
-  // ao -> A planes; LN1(x) -> Av (fp32, the residual of the out-projection): both loads in flight
-  // together, no second read of x later
-  tok_rows<C, TM, ROWS_SPLIT, NW>(P.ao, C, m0, M, nullptr, nullptr, Ah, Al, nullptr, nullptr);
-  tok_rows<C, TM, ROWS_LNF, NW>(P.x, C, m0, M, P.l1w, P.l1b, Ah, Al, nullptr, nullptr, &Av[0][0], VS);
-  __syncthreads();
-
-  floatx16 acc[NT];
-  // av = ao Wo^T + bo + LN1(x)   (models/unet_cond.py:49-50); each Av element is read and
-  // rewritten by the same lane
-  tok_gemm<C, NT, X1>(Ah, Al, P.w0, nw, acc, arow0, fr, fh);
-#pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    const int col = nw + 32 * j + fr;
-    const float bo = P.w0.bias[col];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = arow0 + tok_r(fh, r);
-      Av[row][col] = (acc[j][r] * P.w0.inv_scale + bo) + Av[row][col];
+  if constexpr (WLDS) {
+    constexpr int CPR = C / 8;
+    for (int i = threadIdx.x; i < 3 * C * CPR; i += NW * 64) {
+      const int w = i / (C * CPR), r = (i / CPR) % C, q = i % CPR;
+      const TokW& tw = w == 0 ? P.w0 : w == 1 ? P.w1 : P.w2;
+      const size_t o = (size_t)r * tw.kpad + q * 8;
+      *reinterpret_cast<half8*>(&Wh[w][r][q * 8]) = *reinterpret_cast<const half8*>(tw.h + o);
+      if constexpr (!X1) *reinterpret_cast<half8*>(&Wl[w][r][q * 8]) = *reinterpret_cast<const half8*>(tw.l + o);
     }
   }
-  __syncthreads();
-  // LN2(av) -> A planes (ff_self[0])
-  tok_rows<C, TM, ROWS_LN, NW>(&Av[0][0], VS, 0, TM, P.l2w, P.l2b, Ah, Al, nullptr, nullptr);
-  __syncthreads();
-  // f = GELU(LN2(av) W1^T + b1)  (ff_self[1:3])
-  tok_gemm<C, NT, X1>(Ah, Al, P.w1, nw, acc, arow0, fr, fh);
-  __syncthreads();  // every wave is done reading the LN2 planes
+  auto gemm = [&](int w, const TokW& tw, floatx16(&acc)[NT]) {
+    if constexpr (WLDS) tok_gemm_lds<C, NT, X1>(Ah, Al, Wh[w], Wl[X1 ? 0 : w], nw, acc, arow0, fr, fh);
+    else tok_gemm<C, NT, X1>(Ah, Al, tw, nw, acc, arow0, fr, fh);
+  };
+
+  for (int t = 0; t < TPB; ++t) {
+    const int m0 = (blockIdx.x * TPB + t) * TM;
+    if (m0 >= M) break;
+    // ao -> A planes; LN1(x) -> Av (fp32, the residual of the out-projection): both loads in
+    // flight together, no second read of x later
+    tok_rows<C, TM, ROWS_SPLIT, NW>(P.ao, C, m0, M, nullptr, nullptr, Ah, Al, nullptr, nullptr);
+    tok_rows<C, TM, ROWS_LNF, NW>(P.x, C, m0, M, P.l1w, P.l1b, Ah, Al, nullptr, nullptr, &Av[0][0], VS);
+    __syncthreads();
+
+    floatx16 acc[NT];
+    // av = ao Wo^T + bo + LN1(x)   (models/unet_cond.py:49-50); each Av element is read and
+    // rewritten by the same lane
+    gemm(0, P.w0, acc);
 #pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    const int col = nw + 32 * j + fr;
-    const float b = P.w1.bias[col];
+    for (int j = 0; j < NT; ++j) {
+      const int col = nw + 32 * j + fr;
+      const float bo = P.w0.bias[col];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = arow0 + tok_r(fh, r);
-      const float f = gelu(acc[j][r] * P.w1.inv_scale + b);
-      const _Float16 h = (_Float16)f;
-      Ah[row][col] = h;
-      Al[row][col] = (_Float16)(f - (float)h);
+      for (int r = 0; r < 16; ++r) {
+        const int row = arow0 + tok_r(fh, r);
+        Av[row][col] = (acc[j][r] * P.w0.inv_scale + bo) + Av[row][col];
+      }
     }
-  }
-  __syncthreads();
-  // out = f W2^T + b2 + av  (ff_self[3] + residual, models/unet_cond.py:51)
-  tok_gemm<C, NT, X1>(Ah, Al, P.w2, nw, acc, arow0, fr, fh);
+    __syncthreads();
+    // LN2(av) -> A planes (ff_self[0])
+    tok_rows<C, TM, ROWS_LN, NW>(&Av[0][0], VS, 0, TM, P.l2w, P.l2b, Ah, Al, nullptr, nullptr);
+    __syncthreads();
+    // f = GELU(LN2(av) W1^T + b1)  (ff_self[1:3])
+    gemm(1, P.w1, acc);
+    __syncthreads();  // every wave is done reading the LN2 planes
 #pragma unroll
-  for (int j = 0; j < NT; ++j) {
-    const int col = nw + 32 * j + fr;
-    const float b = P.w2.bias[col];
+    for (int j = 0; j < NT; ++j) {
+      const int col = nw + 32 * j + fr;
+      const float b = P.w1.bias[col];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = arow0 + tok_r(fh, r), m = m0 + row;
-      if (m < M) P.out[(size_t)m * C + col] = (acc[j][r] * P.w2.inv_scale + b) + Av[row][col];
+      for (int r = 0; r < 16; ++r) {
+        const int row = arow0 + tok_r(fh, r);
+        const float f = gelu(acc[j][r] * P.w1.inv_scale + b);
+        const _Float16 h = (_Float16)f;
+        Ah[row][col] = h;
+        Al[row][col] = (_Float16)(f - (float)h);
+      }
     }
+    __syncthreads();
+    // out = f W2^T + b2 + av  (ff_self[3] + residual, models/unet_cond.py:51)
+    gemm(2, P.w2, acc);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int col = nw + 32 * j + fr;
+      const float b = P.w2.bias[col];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = arow0 + tok_r(fh, r), m = m0 + row;
+        if (m < M) P.out[(size_t)m * C + col] = (acc[j][r] * P.w2.inv_scale + b) + Av[row][col];
+      }
+    }
+    if (TPB > 1) __syncthreads();  // the next tile overwrites the planes and Av
   }
 }
 
