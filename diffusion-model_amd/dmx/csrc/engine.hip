@@ -17,6 +17,7 @@
 #include "igemm_x3.h"
 #include "kernels.h"
 #include "igemm_pp.h"
+#include "igemm_ad.h"
 #include "tokmlp.h"
 
 namespace dmx {
@@ -694,17 +695,27 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
     const char* e = std::getenv("DMX_PP_SA0");
     return e ? std::atoi(e) != 0 : false;
   }();
-  const bool pp = x3 && epi == EPI_STATS && cw.phases == 1 && pp_min > 0 && s.C >= 32 &&
+  static const int ad_min = [] {  // A-direct kernel (igemm_ad.h) when its grid has at least this many blocks
+    const char* e = std::getenv("DMX_AD");
+    return e ? std::atoi(e) : 0;
+  }();
+  static const int ad_tmw = [] {  // 32-row fragments per wave of the A-direct kernel (1 | 2)
+    const char* e = std::getenv("DMX_AD_TMW");
+    return (e && std::atoi(e) == 1) ? 1 : 2;
+  }();
+  const bool ad = x3 && epi == EPI_STATS && ad_min > 0 && s.C % 32 == 0 && cw.kpad % 32 == 0 &&
+                  cdiv(M, 128 * ad_tmw) * cdiv(cw.cout, bn) * cw.phases >= ad_min;
+  const bool pp = !ad && x3 && epi == EPI_STATS && cw.phases == 1 && pp_min > 0 && s.C >= 32 &&
                   (ash != nullptr || pp_sa0) && cdiv(M, 256) * cdiv(cw.cout, bn) >= pp_min;
   const bool x3g = x3 && !pp && !x1 && ash != nullptr && glds_enabled() && s.C % 8 == 0;  // LDS-DMA kernel (BK 32)
-  const int bk = (x3g || pp) ? 32 : x1 ? 64 : x3 ? (x3_pipe() == 2 ? 64 : X3_BK) : IG_BK;
+  const int bk = (x3g || pp || ad) ? 32 : x1 ? 64 : x3 ? (x3_pipe() == 2 ? 64 : X3_BK) : IG_BK;
   const int nkt = cw.kpad / bk;
   int splits = 1, ksplit = nkt;
   static const int split_below = [] {  // split K when the grid has fewer blocks than this
     const char* e = std::getenv("DMX_SPLIT_BELOW");
     return e ? std::atoi(e) : 512;  // 2 blocks / CU (measured +1.8 % over 256)
   }();
-  if (!pp && cw.phases == 1 && blocks < split_below && nkt * bk >= 512) {
+  if (!pp && !ad && cw.phases == 1 && blocks < split_below && nkt * bk >= 512) {
     splits = std::min(std::min(8, std::max(2, 512 / blocks)), nkt * bk / 256);
     ksplit = cdiv(nkt, splits);
     splits = cdiv(nkt, ksplit);
@@ -811,6 +822,27 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
     HIPCHK(hipGetLastError());
     return rrows;
   }
+  if (ad) {  // A fragments straight to registers, B through LDS (igemm_ad.h)
+    const int abm = 128 * ad_tmw;
+    dim3 gad(cdiv(M, abm), cdiv(cw.cout, bn), cw.phases);
+    std::snprintf(nm, sizeof nm, "igemm_ad_kernel<%d, %d, %d, %d, %d, 4>", ad_tmw, bn, (int)EPI_STATS, x3_sa,
+                  x1 ? 1 : 0);
+    R.begin(nm, flops, bytes);
+#define ADK(TT, BNN, SAA, XX) igemm_ad_kernel<TT, BNN, EPI_STATS, SAA, XX, 4><<<gad, 256, 0, R.st>>>(xp)
+#define ADK2(TT, BNN)                                        \
+  if (x3_sa) { if (x1) ADK(TT, BNN, 1, 1); else ADK(TT, BNN, 1, 0); } \
+  else { if (x1) ADK(TT, BNN, 0, 1); else ADK(TT, BNN, 0, 0); }
+    if (ad_tmw == 2) {
+      if (bn == 128) { ADK2(2, 128) } else { ADK2(2, 64) }
+    } else {
+      if (bn == 128) { ADK2(1, 128) } else { ADK2(1, 64) }
+    }
+#undef ADK2
+#undef ADK
+    R.end();
+    HIPCHK(hipGetLastError());
+    return rrows;
+  }
   dim3 grid(cdiv(M, bm), cdiv(cw.cout, bn), cw.phases);
   if (x3g) std::snprintf(nm, sizeof nm, "igemm_x3g_kernel<%d, %d, %d, %d>", bm, bn, epi, glds_stages() == 2 ? 2 : 3);
   else if (x3) std::snprintf(nm, sizeof nm, "%s<%d, %d, %d, %d, %d, %d, %d>", kname, bm, bn, epi, bk, x3_nbuf, x3_sa,
@@ -875,10 +907,15 @@ static void norm(Run& R, NormParams np, int N) {
 static void reduce_norm(Run& R, const Deferred& d, NormParams np, int n_src_samples) {
   if (R.plan) return;
   const int n_out = np.n_src > 0 ? 2 * n_src_samples : n_src_samples;
-  R.begin("reduce_norm_kernel", 0.0,
+  const int kv = cdiv(np.HW * (np.C / 4), 1024);
+  const int kvt = kv <= 1 ? 1 : kv <= 2 ? 2 : kv <= 4 ? 4 : RN_MAXV;
+  R.begin("reduce_norm_kernel<" + std::to_string(kvt) + ">", 0.0,
           4.0 * (double)n_src_samples * np.HW * np.C * (d.splits + (np.res ? 1 : 0)) +
               4.0 * (double)n_out * np.HW * np.C * (np.out_h ? 1 : 1));
-  reduce_norm_kernel<<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
+  if (kv <= 1) reduce_norm_kernel<1><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
+  else if (kv <= 2) reduce_norm_kernel<2><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
+  else if (kv <= 4) reduce_norm_kernel<4><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
+  else reduce_norm_kernel<RN_MAXV><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
   R.end();
   HIPCHK(hipGetLastError());
 }

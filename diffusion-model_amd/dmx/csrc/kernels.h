@@ -157,6 +157,38 @@ struct NormParams {
 __global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
   const int n = blockIdx.y, tid = threadIdx.x;
   const int ns = p.n_src > 0 ? n % p.n_src : n;  // source sample (CFG-shared trunk prefix)
+  // This block's float4 range [beg, end) of the sample; chunks are multiples of 256, so when
+  // C/4 divides 256 a thread's channel is loop-invariant.  4 float4 per thread per pass,
+  // every load issued before any is used; the first pass's loads are issued before the
+  // statistics reduction below, which they do not depend on.
+  const int C4 = p.C >> 2;
+  const int per = p.HW * C4;
+  const int chunk = (((per + (int)gridDim.x - 1) / (int)gridDim.x) + 255) & ~255;
+  const int beg = blockIdx.x * chunk, end = min(per, beg + chunk);
+  const size_t base = (size_t)n * per * 4, sbase = (size_t)ns * per * 4;
+  const float* raw = p.raw + sbase;
+  const float* res = p.res != nullptr ? p.res + sbase : nullptr;
+  floatx4 v[4], r[4];
+  auto load = [&](int i0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int idx = min(i0 + 256 * k, end - 1);
+      v[k] = ld4(raw + (size_t)idx * 4);
+      if (res != nullptr) r[k] = ld4(res + (size_t)idx * 4);
+    }
+  };
+  int i0 = beg + tid;
+  if (i0 < end) load(i0);
+  const int cpg = p.C / p.G;
+  const bool cfix = (256 % C4) == 0;
+  const int cthr = (tid % C4) * 4;
+  floatx4 fg{}, fb{}, fe{};  // gamma / beta / emb of a loop-invariant channel, loaded up front
+  if (cfix) {
+    fg = ld4(p.gamma + cthr);
+    fb = ld4(p.beta + cthr);
+    if (p.emb != nullptr) fe = ld4(p.emb + (size_t)n * p.emb_stride + p.emb_off + cthr);
+  }
+
   __shared__ double r1[4], r2[4];
   __shared__ float2 st_s;
   if (p.rowpart != nullptr) {  // GroupNorm(1, C): reduce this sample's (sum, sumsq) partials in double
@@ -164,9 +196,9 @@ __global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
     const float2* rp = p.rowpart + (size_t)ns * cnt;
     double s1 = 0.0, s2 = 0.0;
     for (int i = tid; i < cnt; i += 256) {
-      const float2 v = rp[i];
-      s1 += (double)v.x;
-      s2 += (double)v.y;
+      const float2 q = rp[i];
+      s1 += (double)q.x;
+      s2 += (double)q.y;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -187,34 +219,14 @@ __global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
     }
     __syncthreads();
   }
-  // This block's float4 range [beg, end) of the sample; chunks are multiples of 256, so when
-  // C/4 divides 256 a thread's channel is loop-invariant.  4 float4 per thread per pass,
-  // every load issued before any is used.
-  const int C4 = p.C >> 2;
-  const int per = p.HW * C4;
-  const int chunk = (((per + (int)gridDim.x - 1) / (int)gridDim.x) + 255) & ~255;
-  const int beg = blockIdx.x * chunk, end = min(per, beg + chunk);
-  const size_t base = (size_t)n * per * 4, sbase = (size_t)ns * per * 4;
-  const float* raw = p.raw + sbase;
-  const float* res = p.res != nullptr ? p.res + sbase : nullptr;
-  const int cpg = p.C / p.G;
-  const bool cfix = (256 % C4) == 0;
-  const int cthr = (tid % C4) * 4;
-  for (int i0 = beg + tid; i0 < end; i0 += 1024) {
-    floatx4 v[4], r[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int idx = min(i0 + 256 * k, end - 1);
-      v[k] = ld4(raw + (size_t)idx * 4);
-      if (res != nullptr) r[k] = ld4(res + (size_t)idx * 4);
-    }
+  for (; i0 < end; i0 += 1024) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int idx = i0 + 256 * k;
       if (idx >= end) break;
       const int c = cfix ? cthr : (idx % C4) * 4;
       const float2 st = p.rowpart != nullptr ? st_s : p.stats[ns * p.G + c / cpg];
-      floatx4 o = gn_apply4(v[k], st, p.gamma, p.beta, c, 0);
+      floatx4 o = cfix ? gn_apply4v(v[k], st, fg, fb, 0) : gn_apply4(v[k], st, p.gamma, p.beta, c, 0);
       if (res != nullptr) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] = gelu(r[k][j] + o[j]);
@@ -223,7 +235,7 @@ __global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
         for (int j = 0; j < 4; ++j) o[j] = gelu(o[j]);
       }
       if (p.emb != nullptr) {
-        const floatx4 e = ld4(p.emb + (size_t)n * p.emb_stride + p.emb_off + c);
+        const floatx4 e = cfix ? fe : ld4(p.emb + (size_t)n * p.emb_stride + p.emb_off + c);
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] += e[j];
       }
@@ -236,6 +248,7 @@ __global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
         *reinterpret_cast<half4*>(p.out_l + off) = ll;
       }
     }
+    if (i0 + 1024 < end) load(i0 + 1024);
   }
 }
 
@@ -249,31 +262,41 @@ __global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
 // conv output) at 8x8 / 4x4 where both are launch-latency bound.
 constexpr int RN_MAXV = 8;  // float4 per thread
 
+// KV = float4 per thread (power of two >= ceil(HW*C/4 / 1024)); the split slabs are read SB at
+// a time with every load of a batch in flight together (one memory round trip per batch, not
+// per slab) and summed in split order.  (Loading bias / gamma / beta / residual / emb up
+// front with the first batch was measured slower.)
+template <int KV>
 __global__ __launch_bounds__(1024) void reduce_norm_kernel(const float* partial, int splits, const float* bias,
                                                            const NormParams p) {
+  constexpr int SB = KV >= 16 ? 1 : 16 / KV;  // slabs per batch (<= 64 VGPRs of loads)
   const int s = blockIdx.x, tid = threadIdx.x;
   const int C4 = p.C >> 2, per = p.HW * C4;
   const size_t sstride = (size_t)gridDim.x * per * 4;  // floats per split slab (all source samples)
   const size_t sbase = (size_t)s * per * 4;
-  floatx4 v[RN_MAXV];
+  floatx4 v[KV];
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-  for (int k = 0; k < RN_MAXV; ++k) v[k] = floatx4{0.f, 0.f, 0.f, 0.f};
-  // split-major: each slab's RN_MAXV loads are issued together (one wait per slab, not per load)
-  for (int sp = 0; sp < splits; ++sp) {
-    floatx4 a[RN_MAXV];
+  for (int k = 0; k < KV; ++k) v[k] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int sp0 = 0; sp0 < splits; sp0 += SB) {
+    floatx4 a[SB][KV];
 #pragma unroll
-    for (int k = 0; k < RN_MAXV; ++k) {
-      const int idx = tid + 1024 * k;
-      a[k] = idx < per ? ld4(partial + sp * sstride + sbase + (size_t)idx * 4) : floatx4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int b = 0; b < SB; ++b)
 #pragma unroll
-    for (int k = 0; k < RN_MAXV; ++k)
+      for (int k = 0; k < KV; ++k) {
+        const int idx = tid + 1024 * k;
+        a[b][k] = (sp0 + b < splits && idx < per) ? ld4(partial + (sp0 + b) * sstride + sbase + (size_t)idx * 4)
+                                                  : floatx4{0.f, 0.f, 0.f, 0.f};
+      }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[k][j] += a[k][j];
+    for (int b = 0; b < SB; ++b)
+#pragma unroll
+      for (int k = 0; k < KV; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[k][j] += a[b][k][j];
   }
 #pragma unroll
-  for (int k = 0; k < RN_MAXV; ++k) {
+  for (int k = 0; k < KV; ++k) {
     const int idx = tid + 1024 * k;
     if (idx < per) {
       if (bias != nullptr) {
@@ -320,7 +343,7 @@ __global__ __launch_bounds__(1024) void reduce_norm_kernel(const float* partial,
     const int n = s + q * (p.n_src > 0 ? p.n_src : 0);
     const size_t base = (size_t)n * per * 4;
 #pragma unroll
-    for (int k = 0; k < RN_MAXV; ++k) {
+    for (int k = 0; k < KV; ++k) {
       const int idx = tid + 1024 * k;
       if (idx >= per) break;
       const int c = (idx % C4) * 4;

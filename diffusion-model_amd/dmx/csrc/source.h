@@ -10,14 +10,17 @@ DMX_DEV floatx4 ld4(const float* p) { return *reinterpret_cast<const floatx4*>(p
 
 // GroupNorm affine (+ optional GELU) of 4 channels of one pixel.
 // Reference: nn.GroupNorm (models/unet_cond.py:20,23; models/vae.py:36-48).
-DMX_DEV floatx4 gn_apply4(floatx4 v, float2 st, const float* gamma, const float* beta, int c, int act) {
-  floatx4 g = ld4(gamma + c), b = ld4(beta + c), o;
+DMX_DEV floatx4 gn_apply4v(floatx4 v, float2 st, floatx4 g, floatx4 b, int act) {
+  floatx4 o;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     float y = (v[j] - st.x) * st.y * g[j] + b[j];
     o[j] = act ? gelu(y) : y;
   }
   return o;
+}
+DMX_DEV floatx4 gn_apply4(floatx4 v, float2 st, const float* gamma, const float* beta, int c, int act) {
+  return gn_apply4v(v, st, ld4(gamma + c), ld4(beta + c), act);
 }
 
 // Bilinear x2, align_corners=True (nn.Upsample, models/unet_cond.py:76) of the
