@@ -760,6 +760,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   p.nphase = cw.phases;
   if (s.C != cw.cin) throw Error(DMX_E_INTERNAL, "gemm: source channels != weight channels");
   if (x3 && cw.cin < bk) throw Error(DMX_E_INTERNAL, "gemm: x3 path needs Cin >= K-step");
+  if (ash != nullptr && !x3) throw Error(DMX_E_INTERNAL, "gemm: f16-plane operand needs the split GEMM");
   if (src_mode != SRC_PLAIN && src_mode != SRC_NCHW) throw Error(DMX_E_INTERNAL, "gemm: unsupported source");
   X3Params xp;
   xp.g = p;
@@ -963,8 +964,13 @@ static NormParams norm_params(const float* raw, const float2* rowpart, int nseg,
 // `in` is a plain NHWC tensor (or the NCHW network input for `inc`); it doubles as the residual.
 // n_out > N: the block is computed for N samples and its final GroupNorm (+ emb) writes
 // n_out samples, output n reading sample n % N (the CFG-shared prefix of the trunk).
+// in_h / in_l: `in` is available as f16 hi / lo planes (conv1 then reads those).
+// planes_out: the output only feeds the next ResBlock's conv1 — write it as hi / lo planes
+// (same bytes as fp32) when the split GEMM can use them; *wrote_planes reports the choice.
 static float* resblock(Run& R, const ResW& w, const SrcDesc& in, int mode, int N, int H, int W, bool residual,
-                       const float* emb, int emb_stride, int emb_off, int n_out = 0) {
+                       const float* emb, int emb_stride, int emb_off, int n_out = 0,
+                       const _Float16* in_h = nullptr, const _Float16* in_l = nullptr, bool planes_out = false,
+                       bool* wrote_planes = nullptr) {
   const int M = N * H * W, HW = H * W;
   if (n_out <= 0) n_out = N;
   const int seg = 32;
@@ -976,7 +982,7 @@ static float* resblock(Run& R, const ResW& w, const SrcDesc& in, int mode, int N
   float2* rp2 = R.ws.get<float2>((size_t)M * (w.cout / seg));
   float* out = R.ws.get<float>((size_t)n_out * HW * w.cout);
   Deferred d1, d2;  // split-K convs at low resolution: reduce + GroupNorm in one launch
-  const int rr1 = gemm(R, in, mode, N, H, W, w.c1, EPI_STATS, r1, nullptr, rp1, seg, nullptr, nullptr, &d1);
+  const int rr1 = gemm(R, in, mode, N, H, W, w.c1, EPI_STATS, r1, nullptr, rp1, seg, in_h, in_l, &d1);
   NormParams n1 = norm_params(r1, rp1, w.mid / seg, rr1, w.g1.p, w.b1.p, w.mid, HW, a1);
   n1.act = 1;
   _Float16* a1h = reinterpret_cast<_Float16*>(a1);
@@ -999,6 +1005,14 @@ static float* resblock(Run& R, const ResW& w, const SrcDesc& in, int mode, int N
   n2.emb_stride = emb_stride;
   n2.emb_off = emb_off;
   n2.n_src = n_out > N ? N : 0;
+  const bool pout = planes_out && R.m->prec >= 1 && split_a_enabled() && !R.m->debug && emb == nullptr &&
+                    n_out == N && w.cout >= 64;
+  if (wrote_planes != nullptr) *wrote_planes = pout;
+  if (pout) {  // hi | lo halves of the output buffer, as a1
+    n2.out = nullptr;
+    n2.out_h = reinterpret_cast<_Float16*>(out);
+    n2.out_l = n2.out_h + (size_t)n_out * HW * w.cout;
+  }
   if (d2.fused) reduce_norm(R, d2, n2, N);
   else norm(R, n2, n_out);
   R.tap(R.layer + ".r1", r1, (size_t)M * w.mid);
@@ -1303,10 +1317,13 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
     R.layer = "down" + std::to_string(i + 1) + ".0";
     float* pooled = R.ws.get<float>((size_t)nb * nh * nw * cc);
     prep<SRC_MAXPOOL>(R, mp, pooled, nb, nh, nw, "prep_kernel<2>");
-    float* h0 = resblock(R, m->down[i].r0, plain_src(pooled, cc), SRC_PLAIN, nb, nh, nw, true, nullptr, 0, 0);
+    bool hp = false;
+    float* h0 = resblock(R, m->down[i].r0, plain_src(pooled, cc), SRC_PLAIN, nb, nh, nw, true, nullptr, 0, 0, 0,
+                         nullptr, nullptr, m->down[i].r1.c1.Bh != nullptr, &hp);
     R.layer = "down" + std::to_string(i + 1) + ".1";
+    const _Float16* h0h = hp ? reinterpret_cast<const _Float16*>(h0) : nullptr;
     float* h1 = resblock(R, m->down[i].r1, plain_src(h0, cc), SRC_PLAIN, nb, nh, nw, false, emb, m->hsum,
-                         m->down[i].emb_off, N);
+                         m->down[i].emb_off, N, h0h, hp ? h0h + (size_t)nb * nh * nw * cc : nullptr);
     cc = m->down[i].cout;
     ch = nh;
     cw = nw;
@@ -1314,10 +1331,16 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
     cur = attn_block(R, m->sa[i], h1, N, ch, cw);
   }
   // bottleneck
+  const _Float16 *cur_h = nullptr, *cur_l = nullptr;  // planes of `cur` (between bottleneck blocks)
   for (int i = 0; i < m->nbot; ++i) {
     R.layer = "bot" + std::to_string(i + 1);
-    cur = resblock(R, m->bot[i], plain_src(cur, cc), SRC_PLAIN, N, ch, cw, false, nullptr, 0, 0);
+    bool hp = false;
+    const bool nxt = i + 1 < m->nbot && m->bot[i + 1].c1.Bh != nullptr;  // the last one feeds the upsample
+    cur = resblock(R, m->bot[i], plain_src(cur, cc), SRC_PLAIN, N, ch, cw, false, nullptr, 0, 0, 0, cur_h, cur_l, nxt,
+                   &hp);
     cc = m->bot[i].cout;
+    cur_h = hp ? reinterpret_cast<const _Float16*>(cur) : nullptr;
+    cur_l = hp ? cur_h + (size_t)N * ch * cw * cc : nullptr;
   }
   // up path
   for (int i = 0; i < 3; ++i) {
@@ -1335,10 +1358,13 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
     R.layer = "up" + std::to_string(i + 1) + ".0";
     float* cat = R.ws.get<float>((size_t)N * sh[si] * sw[si] * u.C);
     prep<SRC_UPCAT>(R, u, cat, N, sh[si], sw[si], "prep_kernel<3>");
-    float* h0 = resblock(R, m->up[i].r0, plain_src(cat, u.C), SRC_PLAIN, N, sh[si], sw[si], true, nullptr, 0, 0);
+    bool hp = false;
+    float* h0 = resblock(R, m->up[i].r0, plain_src(cat, u.C), SRC_PLAIN, N, sh[si], sw[si], true, nullptr, 0, 0, 0,
+                         nullptr, nullptr, m->up[i].r1.c1.Bh != nullptr, &hp);
     R.layer = "up" + std::to_string(i + 1) + ".1";
+    const _Float16* h0h = hp ? reinterpret_cast<const _Float16*>(h0) : nullptr;
     float* h1 = resblock(R, m->up[i].r1, plain_src(h0, u.C), SRC_PLAIN, N, sh[si], sw[si], false, emb, m->hsum,
-                         m->up[i].emb_off);
+                         m->up[i].emb_off, 0, h0h, hp ? h0h + (size_t)N * sh[si] * sw[si] * u.C : nullptr);
     ch = sh[si];
     cw = sw[si];
     cc = m->up[i].cout;

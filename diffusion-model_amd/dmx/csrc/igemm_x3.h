@@ -553,6 +553,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     __syncthreads();  // previous chunk fully consumed
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
+#ifdef DMX_DIAG_ATT_NOSTAGE  // diagnostic build only: wrong results, measures the staging cost
+      if (c0 > 0) break;
+#endif
       const int i = tid + 256 * it, key = i / (D / 4), d4 = (i % (D / 4)) * 4;
       const bool kvalid = c0 + key < L;  // keys past L: zero K / V (their scores are masked)
       const floatx4 z = {0.f, 0.f, 0.f, 0.f};
