@@ -34,7 +34,7 @@ def main(fetch_dir, write_dir, out):
             w = sum(wr[k]) / len(wr[k])
             res[k] = {"fetch_kb_raw": f, "write_kb": w, "bytes": 2 * f * 1024 + w * 1024, "launches": len(fe[k])}
     doc = {"method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes of `python3 bench.py "
-                     "--steps 10 --warmup 2 --cpu-steps 0 --no-profile`; bytes/launch = 2*FETCH_SIZE*1024 + "
+                     "--steps 3 --warmup 1 --cpu-steps 0 --config4-steps 0 --config5-steps 0 --no-profile` (tools/prof.sh); bytes/launch = 2*FETCH_SIZE*1024 + "
                      "WRITE_SIZE*1024 (gfx950 FETCH_SIZE = half of wide coalesced reads); averages over all "
                      "launches of the kernel name",
            "traffic_bytes_per_launch": {k: round(v["bytes"]) for k, v in res.items()},
