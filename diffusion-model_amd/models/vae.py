@@ -61,4 +61,10 @@ class VAE(NativeBacked):
         return z, kl.mean()
 
     def forward(self, x):
-        raise NotImplementedError("VAE.forward is the training objective (models/vae.py:71-76) — out of dmx scope")
+        """models/vae.py:71-76, forward only: native encode (same randn_like draw) -> native
+        decode -> recon MSE + 1e-6 * KL, all on x's device.  Returns (x_recon, z, loss,
+        {'recon_mse', 'kl'}).  No autograd graph: VAE training stays out of dmx scope."""
+        z, kl = self.encode(x)
+        x_recon = self.decode(z)
+        recon = torch.nn.functional.mse_loss(x_recon, x.float(), reduction="mean")
+        return x_recon, z, recon + 1e-6 * kl, {"recon_mse": recon.detach(), "kl": kl.detach()}

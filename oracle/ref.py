@@ -165,6 +165,15 @@ def vae_encode(sd: SD, x: torch.Tensor, eps: torch.Tensor, scale_factor: float =
     return z, kl.mean(), mu, logvar
 
 
+def vae_forward(sd: SD, x: torch.Tensor, eps: torch.Tensor, scale_factor: float = 0.18215):
+    """models/vae.py:71-76 (inference form, eps passed in): encode -> decode -> mean-squared
+    reconstruction error + 1e-6 * KL.  Returns (x_recon, z, loss, recon_mse, kl)."""
+    z, kl, _, _ = vae_encode(sd, x, eps, scale_factor)
+    x_recon = vae_decode(sd, z, scale_factor)
+    recon = F.mse_loss(x_recon, x, reduction="mean")
+    return x_recon, z, recon + 1e-6 * kl, recon, kl
+
+
 def to_uint8(img: torch.Tensor) -> torch.Tensor:
     """diff.py:58-62 — x*255 -> clamp(0,255) -> .to(uint8) (truncation)."""
     return (img * 255).clamp(0, 255).to(torch.uint8)

@@ -142,6 +142,22 @@ def test_vae_encode_dropin_draws_like_reference(vae, cuda):
     assert z.shape == (2, 4, 4, 4) and kl.dim() == 0 and torch.isfinite(z).all()
 
 
+def test_vae_forward_vs_oracle(golden, vae, vae_sd, cuda):
+    """Drop-in VAE.forward (models/vae.py:71-76: encode -> decode -> MSE + 1e-6 KL) vs the oracle given
+    the same randn_like draw: x_recon, z and loss rel <= 2e-5."""
+    g = golden("vae_encode.npz")
+    x = torch.from_numpy(g["x64"]).to(cuda)
+    torch.manual_seed(3)
+    with torch.no_grad():
+        x_recon, z, loss, parts = vae(x)
+    torch.manual_seed(3)
+    eps = torch.randn(z.shape, device=cuda).cpu()
+    exp_recon, exp_z, exp_loss, exp_mse, exp_kl = ref.vae_forward(vae_sd, x.cpu(), eps)
+    assert rel(z, exp_z) < TOL and rel(x_recon, exp_recon) < TOL
+    assert abs(float(loss) - float(exp_loss)) <= TOL * abs(float(exp_loss))
+    assert abs(float(parts["kl"]) - float(exp_kl)) <= TOL * abs(float(exp_kl))
+
+
 def test_vae_decode_vs_oracle_odd_batch(vae, cuda, vae_sd):
     z = torch.randn((3, 4, 8, 8), generator=torch.Generator().manual_seed(4))
     with torch.no_grad():

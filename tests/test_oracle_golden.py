@@ -121,3 +121,16 @@ def test_vae_encode(golden, vae_sd, tag):
     assert torch.equal(z, torch.from_numpy(g[f"z{tag}"]))
     assert torch.equal(mu, torch.from_numpy(g[f"mu{tag}"]))
     assert float(kl) == float(g[f"kl{tag}"])
+
+
+def test_vae_forward_composes_encode_decode(golden, vae_sd):
+    """VAE.forward (models/vae.py:71-76) restated as encode -> decode -> MSE + 1e-6 KL; its encode half is
+    pinned by the reference's encode outputs (parity of the loss arithmetic itself is unpinned)."""
+    g = golden("vae_encode.npz")
+    x, eps = torch.from_numpy(g["x64"]), torch.from_numpy(g["eps64"])
+    with torch.no_grad():
+        x_recon, z, loss, recon, kl = ref.vae_forward(vae_sd, x, eps)
+        assert torch.equal(z, torch.from_numpy(g["z64"]))
+        assert float(kl) == float(g["kl64"])
+        assert torch.equal(x_recon, ref.vae_decode(vae_sd, z))
+        assert float(loss) == float(((x_recon - x) ** 2).mean() + 1e-6 * kl)
