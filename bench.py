@@ -43,13 +43,18 @@ def parse():
     ap.add_argument("--hw", type=int, default=32)
     ap.add_argument("--T", type=int, default=1000)
     ap.add_argument("--guidance", type=float, default=3.0)
-    ap.add_argument("--cpu-steps", type=int, default=3, help="oracle steps timed for cpu_baseline (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-steps", type=int, default=5, help="oracle steps timed for cpu_baseline, median (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0: os.cpu_count(), capped by OMP_NUM_THREADS where the host sets the process's share")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--config5-steps", type=int, default=100,
                     help="steps timed in BASELINE config 5 (B=1, VAE decode of every x_t) (0 = skip)")
     ap.add_argument("--config4-steps", type=int, default=100,
                     help="steps timed in BASELINE config 4 (fp16 arithmetic) beside the headline (0 = skip)")
+    ap.add_argument("--legs-steps", type=int, default=30,
+                    help="steps timed for the fp32-MFMA and host-noise legs beside the headline (0 = skip)")
+    ap.add_argument("--png-steps", type=int, default=100,
+                    help="steps of the generate_steps drop-in (async PNG pipeline) timed for config 5 (0 = skip)")
     return ap.parse_args()
 
 
@@ -87,27 +92,84 @@ def make_inputs(B, hw, dev, seed=0):
     return x.to(dev), y.to(dev), vals.to(dev), mask.to(dev)
 
 
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(args):
     """The oracle (reference-equivalent torch-CPU restatement, bit-exact with the reference on this
-    container) timed on the host cores: a bounded sample of CFG steps at the benchmark shape."""
+    container) timed on the host cores: 1 warm-up + the median of --cpu-steps CFG steps at the
+    benchmark shape (BASELINE.md:48-53).  Threads: os.cpu_count(), capped by OMP_NUM_THREADS where
+    the host sets this process's share (16 per GPU on the MI355X pool)."""
     from dmx import synth
     from oracle import ref
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    share = int(os.environ.get("OMP_NUM_THREADS") or 0)
+    threads = args.cpu_threads or min(os.cpu_count() or 1, share or (os.cpu_count() or 1))
     torch.set_num_threads(threads)
     sd = synth.unet_cond_geom_weights(0)
     x, y, vals, mask = make_inputs(args.batch, args.hw, "cpu")
     _, a, ab = ref.schedule(args.T)
     t = torch.full((args.batch,), args.T, dtype=torch.long)
+    times = []
     with torch.no_grad():
         ref.cfg_step(sd, x, t, y, a, ab, args.guidance, 0, vals, mask, torch.randn(x.shape))  # warm-up
-        t0 = time.perf_counter()
         for _ in range(args.cpu_steps):
+            t0 = time.perf_counter()
             x = ref.cfg_step(sd, x, t, y, a, ab, args.guidance, 0, vals, mask, torch.randn(x.shape))
+            times.append(time.perf_counter() - t0)
+    med = sorted(times)[len(times) // 2]
+    return {"value": round(1.0 / med, 4), "unit": "CFG batch-steps/s (B=%d)" % args.batch, "cores": threads,
+            "kind": "port", "cpu_model": _cpu_model(), "host_cpu_count": os.cpu_count(),
+            "sample": f"median of {args.cpu_steps} CFG steps at B={args.batch}, {args.hw}x{args.hw}x4, after 1 "
+                      f"warm-up (oracle/ref.py, torch-CPU fp32, {threads} threads); step times "
+                      f"{[round(v, 3) for v in times]} s"}
+
+
+def legs(nm, model, x, y, vals, mask, args, tables, seed):
+    """Beside the headline: the same config-2 step in exact-fp32 MFMA mode (precision 0, graph
+    replay) and on the default drop-in path (Diffuser.denoise_cond with host CPU-generator noise:
+    one eager dmx_step per step plus the host draw and its H2D copy)."""
+    import diff
+    out = {}
+    k = args.legs_steps
+    with nm.precision_override("fp32"):
+        xs = x.clone()
+        t_dev = torch.full((1,), args.T, dtype=torch.long, device=x.device)
+        nm.sample_loop(xs, t_dev, y, 0, vals, mask, args.guidance, tables, 3, seed=seed)
+        torch.cuda.synchronize()
+        t_dev.fill_(args.T)
+        t0 = time.perf_counter()
+        nm.sample_loop(xs, t_dev, y, 0, vals, mask, args.guidance, tables, k, seed=seed)
+        torch.cuda.synchronize()
         dt = time.perf_counter() - t0
-    return {"value": args.cpu_steps / dt, "unit": "CFG batch-steps/s (B=%d)" % args.batch, "cores": threads,
-            "kind": "port",
-            "sample": f"{args.cpu_steps} CFG steps at B={args.batch}, {args.hw}x{args.hw}x4, after 1 warm-up "
-                      f"(oracle/ref.py, torch-CPU fp32, {threads} threads)"}
+    out["fp32_mfma"] = {"value": round(k / dt, 3), "unit": "CFG batch-steps/s (B=%d)" % args.batch,
+                        "ms_per_step": round(dt / k * 1e3, 4), "steps": k,
+                        "dtype": "f32 (exact fp32 MFMA v_mfma_f32_32x32x2_f32 / 16x16x4_f32)"}
+    d = diff.Diffuser(args.T, device=x.device)
+    xs = x.clone()
+    with torch.no_grad():
+        for i in range(3):
+            xs = d.denoise_cond(model, xs, torch.full((args.batch,), args.T - i, dtype=torch.long, device=x.device),
+                                y=y, guidance_scale=args.guidance, cond_vals=vals, cond_mask=mask)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(k):
+            tt = torch.full((args.batch,), args.T - i, dtype=torch.long, device=x.device)
+            xs = d.denoise_cond(model, xs, tt, y=y, guidance_scale=args.guidance, cond_vals=vals, cond_mask=mask)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    assert torch.isfinite(xs).all(), "non-finite latents (host-noise leg)"
+    out["host_noise"] = {"value": round(k / dt, 3), "unit": "CFG batch-steps/s (B=%d)" % args.batch,
+                         "ms_per_step": round(dt / k * 1e3, 4), "steps": k,
+                         "path": "Diffuser.denoise_cond, torch CPU-generator noise (reference draw order), eager"}
+    return out
 
 
 MFMA_FAMILIES = ("igemm_x3_kernel", "igemm_x3g_kernel", "igemm_pp_kernel", "igemm_ad_kernel", "igemm_f32_kernel",
@@ -208,10 +270,44 @@ def config5(nm, args, tables, seed):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     assert torch.isfinite(x).all(), "non-finite latents (config 5)"
-    return {"workload": "config 5: generate_steps path, B=1, VAE decode (uint8 256x256) of x_t before every CFG step",
-            "value": round(args.config5_steps / dt, 2), "unit": "denoising steps/s (B=1, decode every step)",
-            "ms_per_step": round(dt / args.config5_steps * 1e3, 4), "steps": args.config5_steps, "dtype": "f32 (x3)",
-            "gflop_per_step": round(2 * UNET_GFLOP_PER_SAMPLE + 11.52, 2)}
+    res = {"workload": "config 5: generate_steps path, B=1, VAE decode (uint8 256x256) of x_t before every CFG step",
+           "value": round(args.config5_steps / dt, 2), "unit": "denoising steps/s (B=1, decode every step)",
+           "ms_per_step": round(dt / args.config5_steps * 1e3, 4), "steps": args.config5_steps, "dtype": "f32 (x3)",
+           "gflop_per_step": round(2 * UNET_GFLOP_PER_SAMPLE + 11.52, 2), "png": "excluded (kernels only)"}
+    if args.png_steps > 0:
+        res["with_png"] = config5_png(args, vae)
+    return res
+
+
+def config5_png(args, vae):
+    """The generate_steps.py drop-in end to end (save_reverse_steps_for_csv_row, every step saved:
+    decode + 1 pixel PNG + 4 latent-channel PNGs per step through the async pipeline), both noise
+    sources; PNG encode and file writes included."""
+    import tempfile
+    import generate_steps as gs
+    from dmx import synth
+    from models.unet_cond_geom import UnetCondWithGeomHead
+    dev = torch.device("cuda", torch.cuda.current_device())
+    m = UnetCondWithGeomHead()
+    m.load_state_dict(synth.unet_cond_geom_weights(0))
+    m.to(dev).eval()
+    csv = os.path.join(REPO, "tests", "golden", "entities.csv")
+    out = {}
+    for mode in ("host", "device"):
+        with tempfile.TemporaryDirectory() as tmp:
+            kw = dict(csv_path=csv, row_index=0, class_id=1, model=m, vae=vae, device="cuda",
+                      z_shape=(1, 4, args.hw, args.hw), out_root=tmp, progress=False, noise_source=mode)
+            gs.save_reverse_steps_for_csv_row(num_timesteps=5, run_name="warm", **kw)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            gs.save_reverse_steps_for_csv_row(num_timesteps=args.png_steps, run_name="run", **kw)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            n_png = sum(len(f) for _, _, f in os.walk(os.path.join(tmp, "run")))
+        out[mode + "_noise"] = {"value": round(args.png_steps / dt, 2), "unit": "denoising steps/s incl. 5 PNGs/step",
+                                "ms_per_step": round(dt / args.png_steps * 1e3, 4), "steps": args.png_steps,
+                                "pngs": n_png}
+    return out
 
 
 def config4(nm, x, y, vals, mask, args, tables, seed):
@@ -309,6 +405,8 @@ def main():
         out["config4"] = config4(nm, x, y, vals, mask, args, tables, seed)
     if world == 1 and args.config5_steps > 0:
         out["config5"] = config5(nm, args, tables, seed)
+    if world == 1 and args.legs_steps > 0:
+        out.update(legs(nm, model, x, y, vals, mask, args, tables, seed))
     if rank == 0:
         if not args.no_profile:
             xp = x.clone()

@@ -58,6 +58,7 @@ class Diffuser:
         self._tables: Dict[Tuple[str, bool], Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = {}
         self.noise_source = "host"
         self.use_graph = True
+        self.range_fallbacks = 0  # chunks recomputed in fp32 by the range guard
 
     # ---- schedule tables (per t-1) ---------------------------------------------------------
     def coef_tables(self, device, clamp_prev: bool = True):
@@ -176,16 +177,57 @@ class Diffuser:
         """Latent sampler, unconditional model (diff.py:87-125)."""
         batch_size = z_shape[0]
         x = self._randn(z_shape, self.device)
-        it = range(self.num_timesteps, 0, -1)
-        if progress:
-            it = tqdm(it)
-        with torch.no_grad():
-            for i in it:
+        bar = tqdm(total=self.num_timesteps) if progress else None
+
+        def run(i_from, i_to, x):
+            for i in range(i_from, i_to, -1):
                 t = torch.full((batch_size,), i, device=self.device, dtype=torch.long)
                 x = self.denoise(model, x, t)
+                if bar is not None:
+                    bar.update(1)
+            return x
+
+        with torch.no_grad():
+            x = self._guarded_host_loop(model, x, run)
+        if bar is not None:
+            bar.close()
         if vae is None:
             return x
         return self._decode(vae, x, to_pil)
+
+    # ---- split-precision range guard ------------------------------------------------------
+    GUARD_CHUNK = 50
+
+    @staticmethod
+    def _guard_target(model):
+        """The NativeModel whose range flag guards this loop (None: foreign model or exact fp32)."""
+        if not _native_kind(model):
+            return None
+        nm = model.native()
+        return nm if nm.precision != "fp32" else None
+
+    def _guarded_host_loop(self, model, x, run, on_replay=None):
+        """T steps in chunks of GUARD_CHUNK.  After each chunk the model's range flag is read
+        (dmx_model_range_check); if an operand left the f16 range of the split-precision modes
+        the chunk is replayed from its start — same x, same CPU-generator state, hence the same
+        draws — in exact-fp32 MFMA mode.  `run(i_from, i_to, x)` advances t = i_from .. i_to + 1."""
+        T = self.num_timesteps
+        nm = self._guard_target(model) if x.is_cuda else None
+        i = T
+        while i >= 1:
+            j = max(i - self.GUARD_CHUNK, 0)
+            x0, rng = x, torch.get_rng_state()
+            x = run(i, j, x)
+            if nm is not None and nm.range_tripped():
+                if on_replay is not None:
+                    on_replay()
+                torch.set_rng_state(rng)
+                with nm.precision_override("fp32"):
+                    x = run(i, j, x0)
+                nm.range_tripped()  # clear
+                self.range_fallbacks += 1
+            i = j
+        return x
 
     def sample_cond(self, model, x_shape, y, guidance_scale=0.0, null_label=0):
         """diff.py:165-172."""
@@ -344,9 +386,10 @@ class Diffuser:
         return self._decode(vae, x, to_pil)
 
     def _run_cond_loop(self, model, x, y, vals, msk, guidance_scale, null_label, progress):
-        """The T loop (diff.py:328-344)."""
+        """The T loop (diff.py:328-344), range-guarded in chunks (_guarded_host_loop)."""
         T = self.num_timesteps
         native = _native_kind(model) in (1, 2) and x.is_cuda and guidance_scale and guidance_scale > 0
+        bar = tqdm(total=T, desc="Sampling (cond+numeric)") if progress else None
         if native and self.noise_source == "device":
             # whole loop on the device: Philox noise, hipGraph replay, t decremented in-graph
             nm = model.native()
@@ -354,25 +397,41 @@ class Diffuser:
             t_dev = torch.full((1,), T, device=x.device, dtype=torch.long)
             tables = self.coef_tables(x.device, clamp_prev=True)
             seed = self._seed()
-            bar = tqdm(total=T, desc="Sampling (cond+numeric)") if progress else None
+            v, m = vals.float().contiguous(), msk.float().contiguous()
+            guard = self._guard_target(model)
             done = 0
             with torch.no_grad():
                 while done < T:
-                    k = min(50, T - done)
-                    nm.sample_loop(x, t_dev, y, null_label, vals.float().contiguous(), msk.float().contiguous(),
-                                   float(guidance_scale), tables, k, seed=seed, use_graph=self.use_graph)
+                    k = min(self.GUARD_CHUNK, T - done)
+                    x0 = x.clone() if guard is not None else None
+                    nm.sample_loop(x, t_dev, y, null_label, v, m, float(guidance_scale), tables, k, seed=seed,
+                                   use_graph=self.use_graph)
+                    if guard is not None and guard.range_tripped():
+                        x.copy_(x0)
+                        t_dev.fill_(T - done)
+                        with guard.precision_override("fp32"):
+                            nm.sample_loop(x, t_dev, y, null_label, v, m, float(guidance_scale), tables, k,
+                                           seed=seed, use_graph=self.use_graph)
+                        guard.range_tripped()
+                        self.range_fallbacks += 1
                     done += k
                     if bar is not None:
                         bar.update(k)
             if bar is not None:
                 bar.close()
             return x
-        it: Iterable[int] = range(T, 0, -1)
-        if progress:
-            it = tqdm(it, desc="Sampling (cond+numeric)")
-        with torch.no_grad():
-            for i in it:
+
+        def run(i_from, i_to, x):
+            for i in range(i_from, i_to, -1):
                 t = torch.full((x.shape[0],), i, device=x.device, dtype=torch.long)
                 x = self.denoise_cond(model=model, x=x, t=t, y=y, guidance_scale=guidance_scale,
                                       null_label=null_label, cond_vals=vals, cond_mask=msk)
+                if bar is not None:
+                    bar.update(1)
+            return x
+
+        with torch.no_grad():
+            x = self._guarded_host_loop(model, x, run)
+        if bar is not None:
+            bar.close()
         return x

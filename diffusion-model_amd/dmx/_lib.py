@@ -47,6 +47,19 @@ class StepArgs(ctypes.Structure):
     ]
 
 
+class ModelConfig(ctypes.Structure):
+    """dmx_model_config (include/dmx.h): reference constructor arguments that shape the network."""
+    _fields_ = [("kind", ctypes.c_int), ("in_ch", ctypes.c_int), ("remove_deep_conv", ctypes.c_int),
+                ("num_classes", ctypes.c_int), ("geom_dim", ctypes.c_int), ("geom_hidden", ctypes.c_int),
+                ("scale_factor", ctypes.c_float)]
+
+    @classmethod
+    def make(cls, kind: int, in_ch: int = 4, remove_deep_conv: bool = False, num_classes: int = 3,
+             geom_dim: int = 12, geom_hidden: int = 256, scale_factor: float = 0.18215) -> "ModelConfig":
+        return cls(int(kind), int(in_ch), int(bool(remove_deep_conv)), int(num_classes), int(geom_dim),
+                   int(geom_hidden), float(scale_factor))
+
+
 class KernelRecord(ctypes.Structure):
     _fields_ = [("kernel", ctypes.c_char * 96), ("layer", ctypes.c_char * 48), ("flops", ctypes.c_double),
                 ("bytes", ctypes.c_double), ("ms", ctypes.c_float)]
@@ -65,17 +78,23 @@ SIGNATURES = [
     ("dmx_model_num_keys", _I, [_I, _I, _I]),
     ("dmx_model_key", _I, [_I, _I, _I, _I, ctypes.c_char_p, _I, ctypes.POINTER(_I64), ctypes.POINTER(_I)]),
     ("dmx_model_create", _I, [_P, _I, _I, _I, ctypes.POINTER(_P)]),
+    ("dmx_model_create_cfg", _I, [_P, ctypes.POINTER(ModelConfig), ctypes.POINTER(_P)]),
+    ("dmx_model_cfg_num_keys", _I, [ctypes.POINTER(ModelConfig)]),
+    ("dmx_model_cfg_key", _I, [ctypes.POINTER(ModelConfig), _I, ctypes.c_char_p, _I, ctypes.POINTER(_I64),
+                               ctypes.POINTER(_I)]),
     ("dmx_model_destroy", _I, [_P]),
     ("dmx_model_set_tensor", _I, [_P, ctypes.c_char_p, _P, ctypes.POINTER(_I64), _I]),
     ("dmx_model_finalize", _I, [_P, _P]),
     ("dmx_model_set_precision", _I, [_P, _I]),
     ("dmx_model_get_precision", _I, [_P]),
+    ("dmx_model_range_check", _I, [_P, _I, ctypes.POINTER(_I), _P]),
     ("dmx_unet_forward", _I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P]),
     ("dmx_step", _I, [_P, ctypes.POINTER(StepArgs), _P]),
     ("dmx_sample_loop", _I, [_P, ctypes.POINTER(StepArgs), _I, _I, _P]),
     ("dmx_ddpm_update", _I, [_P, _P, _P, _P, ctypes.c_float, _P, _I, _P, _P, _P, _I, _P, ctypes.c_uint64, _I64,
                              _I, _I, _I, _I, _P]),
     ("dmx_vae_decode", _I, [_P, _P, _P, _P, _I, _I, _I, _P]),
+    ("dmx_latent_frames_u8", _I, [_P, _P, _I, _I, _I, _I, _P]),
     ("dmx_vae_encode", _I, [_P, _P, _P, _P, _P, _I, _I, _I, _P]),
     ("dmx_model_workspace_bytes", _I64, [_P]),
     ("dmx_debug_enable", _I, [_P, _I]),
@@ -115,15 +134,19 @@ def check(rc: int) -> None:
         raise DmxError(rc, msg.decode() if msg else "")
 
 
-def model_keys(kind: int, in_ch: int = 4, remove_deep_conv: bool = False):
-    """Reference state_dict keys the native loader expects (no GPU needed)."""
+def model_keys(kind: int, in_ch: int = 4, remove_deep_conv: bool = False, **cfg):
+    """Reference state_dict keys the native loader expects (no GPU needed); ``cfg`` takes the
+    other ModelConfig fields (num_classes, geom_dim, geom_hidden, scale_factor)."""
     lib = load()
-    n = lib.dmx_model_num_keys(kind, in_ch, int(remove_deep_conv))
+    c = ModelConfig.make(kind, in_ch, remove_deep_conv, **cfg)
+    n = lib.dmx_model_cfg_num_keys(ctypes.byref(c))
+    if n < 0:
+        raise DmxError(DMX_E_ARG, lib.dmx_last_error().decode())
     out = []
     buf = ctypes.create_string_buffer(256)
     shape = (ctypes.c_int64 * 4)()
     nd = ctypes.c_int()
     for i in range(n):
-        check(lib.dmx_model_key(kind, in_ch, int(remove_deep_conv), i, buf, 256, shape, ctypes.byref(nd)))
+        check(lib.dmx_model_cfg_key(ctypes.byref(c), i, buf, 256, shape, ctypes.byref(nd)))
         out.append((buf.value.decode(), tuple(shape[j] for j in range(nd.value))))
     return out

@@ -17,7 +17,7 @@
 #include "igemm_x3.h"
 #include "kernels.h"
 #include "igemm_pp.h"
-#include "igemm_ad.h"
+#include "launch.h"
 #include "tokmlp.h"
 
 namespace dmx {
@@ -100,7 +100,18 @@ static std::vector<Topo> unet_topo(int in_ch, bool deep) {
   return t;
 }
 
-static Keys model_keys(int kind, int in_ch, bool deep) {
+// Constructor arguments of the reference networks that change the checkpoint layout.
+struct ModelCfg {
+  int kind = 0, in_ch = 4;
+  bool deep = true;
+  int ncls = 4;          // class_emb rows = num_classes + 1 (models/unet_cond.py:121)
+  int gdim = 12, ghid = 256;  // GeomHead (models/unet_cond_geom.py:38-39,49)
+  float scale = 0.18215f;     // VAE scale_factor (models/vae.py:11)
+};
+
+static Keys model_keys(const ModelCfg& c) {
+  const int kind = c.kind, in_ch = c.in_ch;
+  const bool deep = c.deep;
   Keys k;
   if (kind == DMX_VAE) {
     // models/vae.py:17-49
@@ -131,7 +142,7 @@ static Keys model_keys(int kind, int in_ch, bool deep) {
   }
   const bool cond = kind == DMX_UNET_COND_GEOM || kind == DMX_UNET_COND;
   if (cond) {
-    k.push_back({"class_emb.weight", {4, 256}});
+    k.push_back({"class_emb.weight", {c.ncls, 256}});
     k_lin(k, "cond_mlp.0", 24, 256);
     k_lin(k, "cond_mlp.2", 256, 256);
   }
@@ -152,8 +163,8 @@ static Keys model_keys(int kind, int in_ch, bool deep) {
   k.push_back({"out.weight", {in_ch, 64, 1, 1}});
   k.push_back({"out.bias", {in_ch}});
   if (kind == DMX_UNET_COND_GEOM) {
-    k_lin(k, "geom_head.mlp.0", 64, 256);
-    k_lin(k, "geom_head.mlp.2", 256, 12);
+    k_lin(k, "geom_head.mlp.0", 64, c.ghid);
+    k_lin(k, "geom_head.mlp.2", c.ghid, c.gdim);
   }
   return k;
 }
@@ -203,7 +214,7 @@ struct Arena {
 
 struct GraphKey {
   dmx_step_args a;
-  int steps_unused;
+  int table_gen;  // dmx_ctx::table_gen at capture
   bool operator==(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(GraphKey)) == 0; }
 };
 
@@ -213,12 +224,14 @@ struct dmx_ctx {
   int device = 0;
   float* pos_table = nullptr;
   int tmax = 0;
+  int table_gen = 0;  // bumped whenever pos_table is reallocated (captured graphs hold the old pointer)
 };
 
 struct dmx_model {
   dmx_ctx* ctx = nullptr;
   int kind = 0, in_ch = 4;
   bool deep = true;
+  dmx::ModelCfg cfg;
   bool finalized = false;
   dmx::Keys keys;
   std::map<std::string, std::pair<const float*, std::vector<int64_t>>> inputs;
@@ -250,6 +263,7 @@ struct dmx_model {
   // debug taps: (name, device pointer into the workspace, element count, C)
   bool debug = false;
   int prec = 1;  // 0: fp32 MFMA (exact fp32 products), 1: fp16 hi/lo x3 split MFMA, 2: fp16 (config 4)
+  int* range_flag = nullptr;  // device int: an output went non-finite (kernels.h flag_nonfinite)
   std::vector<std::pair<std::string, std::pair<const float*, size_t>>> taps;
 };
 
@@ -503,6 +517,13 @@ static void finalize_model(dmx_model* m, hipStream_t st) {
       m->gb2 = P.copy("geom_head.mlp.2.bias");
     }
   }
+  {
+    void* f = nullptr;
+    HIPCHK(hipMalloc(&f, 256));
+    m->owned.push_back(f);
+    m->range_flag = static_cast<int*>(f);
+    HIPCHK(hipMemsetAsync(f, 0, 256, st));
+  }
   HIPCHK(hipStreamSynchronize(st));
   m->inputs.clear();  // caller's tensors are no longer referenced
   m->finalized = true;
@@ -555,122 +576,20 @@ void Run::tap(const std::string& name, const float* p, size_t count) {
   m->taps.push_back({name, {p, count}});
 }
 
-template <int BM, int BN, int SRC, int EPI>
-static void launch_ig(const IgemmParams& p, dim3 grid, hipStream_t st) {
-  igemm_f32_kernel<BM, BN, SRC, EPI><<<grid, 256, 0, st>>>(p);
-}
+// Mid-ResBlock activation emitted as fp16 hi/lo planes for the split GEMM.
+static bool split_a_enabled() { return true; }
 
-template <int SRC, int EPI>
-static void launch_ig_tiles(int bm, int bn, const IgemmParams& p, dim3 grid, hipStream_t st) {
-  if (bm == 128 && bn == 128) launch_ig<128, 128, SRC, EPI>(p, grid, st);
-  else if (bm == 128) launch_ig<128, 64, SRC, EPI>(p, grid, st);
-  else if (bn == 128) launch_ig<64, 128, SRC, EPI>(p, grid, st);
-  else launch_ig<64, 64, SRC, EPI>(p, grid, st);
-}
-
-// Pipeline variant of the x3 GEMM (A/B experiments; DMX_X3_PIPE env: 0 = BK32 x 2 LDS buffers,
-// 1 = BK32 x 1 buffer, 2 = BK64 x 1 buffer).
-static int x3_pipe() {
-  static int v = [] {
-    const char* e = std::getenv("DMX_X3_PIPE");
-    return e ? std::atoi(e) : 2;
-  }();
-  return v;
-}
-
-// Mid-ResBlock activation emitted as fp16 hi/lo planes for the split GEMM (DMX_SPLIT_A=0 disables).
-static bool split_a_enabled() {
-  static bool v = [] {
-    const char* e = std::getenv("DMX_SPLIT_A");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  return v;
-}
-
-template <int EPI, int BK, int NB, int SA, int X1 = 0>
-static void launch_x3_s(int bm, int bn, const X3Params& p, dim3 grid, hipStream_t st) {
-  if (bm == 128 && bn == 128) igemm_x3_kernel<128, 128, EPI, BK, NB, SA, X1><<<grid, 256, 0, st>>>(p);
-  else if (bm == 128) igemm_x3_kernel<128, 64, EPI, BK, NB, SA, X1><<<grid, 256, 0, st>>>(p);
-  else if (bn == 128) igemm_x3_kernel<64, 128, EPI, BK, NB, SA, X1><<<grid, 256, 0, st>>>(p);
-  else igemm_x3_kernel<64, 64, EPI, BK, NB, SA, X1><<<grid, 256, 0, st>>>(p);
-}
-
-template <int EPI, int BK, int NB, int X1 = 0>
-static void launch_x3_v(int bm, int bn, const X3Params& p, dim3 grid, hipStream_t st) {
-  if (p.Ash != nullptr) launch_x3_s<EPI, BK, NB, 1, X1>(bm, bn, p, grid, st);
-  else launch_x3_s<EPI, BK, NB, 0, X1>(bm, bn, p, grid, st);
-}
-
-// LDS-DMA pipeline for split-plane A operands, opt-in (DMX_GLDS=1; DMX_GLDS_ST=2|3 stages).
-// Measured on MI355X at this model's shapes it trails the register-staged BK64 kernel by
-// 2-4 % (2 stages: DMA latency exposed at each barrier; 3 stages at 128x128: one block / CU).
-static bool glds_enabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("DMX_GLDS");
-    return e ? std::atoi(e) != 0 : false;
-  }();
-  return v;
-}
-
-static int glds_stages() {
-  static const int v = [] {
-    const char* e = std::getenv("DMX_GLDS_ST");
-    return e ? std::atoi(e) : 3;
-  }();
-  return v;
-}
-
-template <int EPI, int NST>
-static void launch_x3g_s(int bm, int bn, const X3Params& p, dim3 grid, hipStream_t st) {
-  if (bm == 128 && bn == 128) igemm_x3g_kernel<128, 128, EPI, NST><<<grid, 256, 0, st>>>(p);
-  else if (bm == 128) igemm_x3g_kernel<128, 64, EPI, NST><<<grid, 256, 0, st>>>(p);
-  else if (bn == 128) igemm_x3g_kernel<64, 128, EPI, NST><<<grid, 256, 0, st>>>(p);
-  else igemm_x3g_kernel<64, 64, EPI, NST><<<grid, 256, 0, st>>>(p);
-}
-
-template <int EPI>
-static void launch_x3g(int bm, int bn, const X3Params& p, dim3 grid, hipStream_t st) {
-  if (glds_stages() == 2) launch_x3g_s<EPI, 2>(bm, bn, p, grid, st);
-  else launch_x3g_s<EPI, 3>(bm, bn, p, grid, st);
-}
-
-template <int EPI>
-static void launch_x3_tiles(int bm, int bn, const X3Params& p, dim3 grid, hipStream_t st, bool x1) {
-  if (x1) {  // config-4 fp16 arithmetic: BK 64, register-staged pipeline only
-    launch_x3_v<EPI, 64, 1, 1>(bm, bn, p, grid, st);
-    return;
-  }
-  if (p.Ash != nullptr && glds_enabled() && p.g.src.C % 8 == 0) {
-    launch_x3g<EPI>(bm, bn, p, grid, st);
-    return;
-  }
-  switch (x3_pipe()) {
-    case 1: launch_x3_v<EPI, 32, 1>(bm, bn, p, grid, st); break;
-    case 2: launch_x3_v<EPI, 64, 1>(bm, bn, p, grid, st); break;
-    default: launch_x3_v<EPI, 32, 2>(bm, bn, p, grid, st); break;
-  }
-}
-
-// Implicit GEMM: conv3x3 (taps 9), ConvT phases (taps 4, phases 4), linear (taps 1).
-// Sources are plain NHWC (or the NCHW network input); grids too small to fill the
-// 256 CUs are split along K into deterministic slabs reduced by splitk_reduce_kernel.
+// Implicit GEMM: conv3x3 (taps 9), ConvT phases (taps 4, phases 4), conv4x4-s2 (taps 16),
+// linear (taps 1).  Sources are plain NHWC (or the NCHW network input); grids too small to
+// fill the 256 CUs are split along K into deterministic slabs reduced by splitk_reduce_kernel
+// (or, in a ResBlock, by the caller's fused reduce_norm_kernel).
 // Returns the GroupNorm partial rows per sample it wrote (EPI_STATS).
-// `defer` (EPI_STATS only): when the GEMM splits K and one sample fits reduce_norm_kernel,
-// the reduce launch is skipped and the slab handed back (defer->fused) for the caller's
-// fused split-K reduce + GroupNorm.
 struct Deferred {
   bool fused = false;
   float* partial = nullptr;
   int splits = 0;
   const float* bias = nullptr;
 };
-static bool reduce_norm_enabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("DMX_REDUCE_NORM");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  return v;
-}
 
 static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, const ConvW& cw, int epi, float* out,
                 const float* res, float2* rowpart, int seg, const _Float16* ash = nullptr,
@@ -678,44 +597,18 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   const int M = N * H * W;
   if (cw.cout % 32 != 0) throw Error(DMX_E_INTERNAL, "gemm: Cout must be a multiple of 32");
   const int bn = (cw.cout % 128 == 0) ? 128 : 64;
-  static const int bm128_min = [] {  // 128-row tiles (split K if the grid is then small) from this many tiles
-    const char* e = std::getenv("DMX_BM128_MIN");
-    return e ? std::atoi(e) : 256;  // measured +0.6 % over 512 (8x8x512 and 32x32x128 layers split in 2)
-  }();
   const int tiles128 = cdiv(M, 128) * cdiv(cw.cout, bn) * cw.phases;
-  const int bm = tiles128 >= bm128_min ? 128 : 64;
+  const int bm = tiles128 >= 256 ? 128 : 64;  // 128-row tiles (split K if the grid is then small) from 256 tiles
   const int blocks = cdiv(M, bm) * cdiv(cw.cout, bn) * cw.phases;
   const bool x3 = R.m->prec >= 1 && src_mode == SRC_PLAIN && cw.Bh != nullptr;
   const bool x1 = x3 && R.m->prec == 2;  // config-4 fp16: one MFMA on the hi planes
-  static const int pp_min = [] {  // ping-pong 256-row kernel when its grid has at least this many blocks
-    const char* e = std::getenv("DMX_PP_MIN");
-    return e ? std::atoi(e) : 256;
-  }();
-  static const bool pp_sa0 = [] {  // also for fp32 A sources (split while staging)
-    const char* e = std::getenv("DMX_PP_SA0");
-    return e ? std::atoi(e) != 0 : false;
-  }();
-  static const int ad_min = [] {  // A-direct kernel (igemm_ad.h) when its grid has at least this many blocks
-    const char* e = std::getenv("DMX_AD");
-    return e ? std::atoi(e) : 0;
-  }();
-  static const int ad_tmw = [] {  // 32-row fragments per wave of the A-direct kernel (1 | 2)
-    const char* e = std::getenv("DMX_AD_TMW");
-    return (e && std::atoi(e) == 1) ? 1 : 2;
-  }();
-  const bool ad = x3 && epi == EPI_STATS && ad_min > 0 && s.C % 32 == 0 && cw.kpad % 32 == 0 &&
-                  cdiv(M, 128 * ad_tmw) * cdiv(cw.cout, bn) * cw.phases >= ad_min;
-  const bool pp = !ad && x3 && epi == EPI_STATS && cw.phases == 1 && pp_min > 0 && s.C >= 32 &&
-                  (ash != nullptr || pp_sa0) && cdiv(M, 256) * cdiv(cw.cout, bn) >= pp_min;
-  const bool x3g = x3 && !pp && !x1 && ash != nullptr && glds_enabled() && s.C % 8 == 0;  // LDS-DMA kernel (BK 32)
-  const int bk = (x3g || pp || ad) ? 32 : x1 ? 64 : x3 ? (x3_pipe() == 2 ? 64 : X3_BK) : IG_BK;
+  // 512-thread ping-pong kernel (256-row tiles) for the large f16-plane convs
+  const bool pp = x3 && epi == EPI_STATS && cw.phases == 1 && s.C >= 32 && ash != nullptr &&
+                  cdiv(M, 256) * cdiv(cw.cout, bn) >= 256;
+  const int bk = pp ? 32 : x3 ? 64 : IG_BK;
   const int nkt = cw.kpad / bk;
   int splits = 1, ksplit = nkt;
-  static const int split_below = [] {  // split K when the grid has fewer blocks than this
-    const char* e = std::getenv("DMX_SPLIT_BELOW");
-    return e ? std::atoi(e) : 512;  // 2 blocks / CU (measured +1.8 % over 256)
-  }();
-  if (!pp && !ad && cw.phases == 1 && blocks < split_below && nkt * bk >= 512) {
+  if (!pp && cw.phases == 1 && blocks < 512 && nkt * bk >= 512) {  // split K below 2 blocks / CU
     splits = std::min(std::min(8, std::max(2, 512 / blocks)), nkt * bk / 256);
     ksplit = cdiv(nkt, splits);
     splits = cdiv(nkt, ksplit);
@@ -724,7 +617,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   const int rgrp = (splits == 1 && (H * W) % 32 == 0) ? 32 : 1;
   const int rrows = cw.phases * H * W / rgrp;
   if (defer != nullptr) {
-    defer->fused = splits > 1 && epi == EPI_STATS && reduce_norm_enabled() && !R.m->debug &&
+    defer->fused = splits > 1 && epi == EPI_STATS && !R.m->debug &&
                    H * W * (cw.cout / 4) <= RN_MAXV * 1024;  // (debug taps read the raw conv output)
     defer->partial = partial;
     defer->splits = splits;
@@ -778,23 +671,25 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
     xp.b_bytes = (unsigned)bb;
   }
   // labels are the demangled kernel names rocprofv3 reports (profiles/ cross-check)
-  const char* kname = x3 ? "igemm_x3_kernel" : "igemm_f32_kernel";
-  const int x3_nbuf = (x1 || x3_pipe() == 1 || x3_pipe() == 2) ? 1 : 2, x3_sa = ash != nullptr ? 1 : 0;
+  const int sa = ash != nullptr ? 1 : 0;
   const int creal = (src_mode == SRC_NCHW && s.C0) ? s.C0 : cw.cin;
   const double flops = 2.0 * (double)M * cw.phases * cw.cout * (double)cw.taps * creal;
   const double bytes = 4.0 * ((double)M * cw.phases * cw.cout + (double)N * p.Hin * p.Win * s.C +
                               (double)cw.phases * cw.cout * cw.taps * cw.cin);
   char nm[96];
+  auto name_x3 = [&](int e) {
+    std::snprintf(nm, sizeof nm, "igemm_x3_kernel<%d, %d, %d, 64, 1, %d, %d>", bm, bn, e, sa, x1 ? 1 : 0);
+  };
+  auto name_f32 = [&](int e) {
+    std::snprintf(nm, sizeof nm, "igemm_f32_kernel<%d, %d, %d, %d>", bm, bn, src_mode, e);
+  };
   if (splits > 1) {
     dim3 grid(cdiv(M, bm), cdiv(cw.cout, bn), splits);
-    if (x3g) std::snprintf(nm, sizeof nm, "igemm_x3g_kernel<%d, %d, %d, %d>", bm, bn, (int)EPI_PARTIAL, glds_stages() == 2 ? 2 : 3);
-    else if (x3) std::snprintf(nm, sizeof nm, "%s<%d, %d, %d, %d, %d, %d, %d>", kname, bm, bn, (int)EPI_PARTIAL, bk,
-                               x3_nbuf, x3_sa, x1 ? 1 : 0);
-    else std::snprintf(nm, sizeof nm, "%s<%d, %d, %d, %d>", kname, bm, bn, src_mode, (int)EPI_PARTIAL);
+    if (x3) name_x3(EPI_PARTIAL);
+    else name_f32(EPI_PARTIAL);
     R.begin(nm, flops, bytes + 4.0 * splits * M * cw.cout);
-    if (x3) launch_x3_tiles<EPI_PARTIAL>(bm, bn, xp, grid, R.st, x1);
-    else if (src_mode == SRC_NCHW) launch_ig_tiles<SRC_NCHW, EPI_PARTIAL>(bm, bn, p, grid, R.st);
-    else launch_ig_tiles<SRC_PLAIN, EPI_PARTIAL>(bm, bn, p, grid, R.st);
+    if (x3) launch_x3_partial(bm, bn, sa, x1 ? 1 : 0, xp, grid, R.st);
+    else launch_f32(src_mode, EPI_PARTIAL, bm, bn, p, grid, R.st);
     R.end();
     HIPCHK(hipGetLastError());
     if (defer != nullptr && defer->fused) return rrows;  // the caller's reduce_norm_kernel sums the slabs
@@ -808,69 +703,25 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   }
   if (pp) {  // 512-thread ping-pong kernel, 256 x bn tiles (igemm_pp.h)
     dim3 gpp(cdiv(M, 256), cdiv(cw.cout, bn), 1);
-    std::snprintf(nm, sizeof nm, "igemm_pp_kernel<%d, %d, %d, %d>", bn, (int)EPI_STATS, x3_sa, x1 ? 1 : 0);
+    std::snprintf(nm, sizeof nm, "igemm_pp_kernel<%d, %d, %d, %d>", bn, (int)EPI_STATS, sa, x1 ? 1 : 0);
     R.begin(nm, flops, bytes);
-#define PPK(BNN, SAA, XX) igemm_pp_kernel<BNN, EPI_STATS, SAA, XX><<<gpp, 512, 0, R.st>>>(xp)
-    if (bn == 128) {
-      if (x3_sa) { if (x1) PPK(128, 1, 1); else PPK(128, 1, 0); }
-      else { if (x1) PPK(128, 0, 1); else PPK(128, 0, 0); }
-    } else {
-      if (x3_sa) { if (x1) PPK(64, 1, 1); else PPK(64, 1, 0); }
-      else { if (x1) PPK(64, 0, 1); else PPK(64, 0, 0); }
-    }
-#undef PPK
-    R.end();
-    HIPCHK(hipGetLastError());
-    return rrows;
-  }
-  if (ad) {  // A fragments straight to registers, B through LDS (igemm_ad.h)
-    const int abm = 128 * ad_tmw;
-    dim3 gad(cdiv(M, abm), cdiv(cw.cout, bn), cw.phases);
-    std::snprintf(nm, sizeof nm, "igemm_ad_kernel<%d, %d, %d, %d, %d, 4>", ad_tmw, bn, (int)EPI_STATS, x3_sa,
-                  x1 ? 1 : 0);
-    R.begin(nm, flops, bytes);
-#define ADK(TT, BNN, SAA, XX) igemm_ad_kernel<TT, BNN, EPI_STATS, SAA, XX, 4><<<gad, 256, 0, R.st>>>(xp)
-#define ADK2(TT, BNN)                                        \
-  if (x3_sa) { if (x1) ADK(TT, BNN, 1, 1); else ADK(TT, BNN, 1, 0); } \
-  else { if (x1) ADK(TT, BNN, 0, 1); else ADK(TT, BNN, 0, 0); }
-    if (ad_tmw == 2) {
-      if (bn == 128) { ADK2(2, 128) } else { ADK2(2, 64) }
-    } else {
-      if (bn == 128) { ADK2(1, 128) } else { ADK2(1, 64) }
-    }
-#undef ADK2
-#undef ADK
+    launch_pp(bn, sa, x1 ? 1 : 0, xp, gpp, R.st);
     R.end();
     HIPCHK(hipGetLastError());
     return rrows;
   }
   dim3 grid(cdiv(M, bm), cdiv(cw.cout, bn), cw.phases);
-  if (x3g) std::snprintf(nm, sizeof nm, "igemm_x3g_kernel<%d, %d, %d, %d>", bm, bn, epi, glds_stages() == 2 ? 2 : 3);
-  else if (x3) std::snprintf(nm, sizeof nm, "%s<%d, %d, %d, %d, %d, %d, %d>", kname, bm, bn, epi, bk, x3_nbuf, x3_sa,
-                             x1 ? 1 : 0);
-  else std::snprintf(nm, sizeof nm, "%s<%d, %d, %d, %d>", kname, bm, bn, epi == EPI_STATS ? src_mode : SRC_PLAIN, epi);
+  if (x3) name_x3(epi);
+  else name_f32(epi == EPI_STATS ? epi : epi);
   R.begin(nm, flops, bytes);
   if (x3) {
-    switch (epi) {
-      case EPI_STATS: launch_x3_tiles<EPI_STATS>(bm, bn, xp, grid, R.st, x1); break;
-      case EPI_BIAS: launch_x3_tiles<EPI_BIAS>(bm, bn, xp, grid, R.st, x1); break;
-      case EPI_BIAS_GELU: launch_x3_tiles<EPI_BIAS_GELU>(bm, bn, xp, grid, R.st, x1); break;
-      case EPI_BIAS_RES: launch_x3_tiles<EPI_BIAS_RES>(bm, bn, xp, grid, R.st, x1); break;
-      default: throw Error(DMX_E_INTERNAL, "bad epilogue");
-    }
-    R.end();
-    HIPCHK(hipGetLastError());
-    return rrows;
-  }
-  switch (epi) {
-    case EPI_STATS:
-      if (src_mode == SRC_NCHW) launch_ig_tiles<SRC_NCHW, EPI_STATS>(bm, bn, p, grid, R.st);
-      else launch_ig_tiles<SRC_PLAIN, EPI_STATS>(bm, bn, p, grid, R.st);
-      break;
-    case EPI_BIAS: launch_ig_tiles<SRC_PLAIN, EPI_BIAS>(bm, bn, p, grid, R.st); break;
-    case EPI_BIAS_GELU: launch_ig_tiles<SRC_PLAIN, EPI_BIAS_GELU>(bm, bn, p, grid, R.st); break;
-    case EPI_BIAS_RES: launch_ig_tiles<SRC_PLAIN, EPI_BIAS_RES>(bm, bn, p, grid, R.st); break;
-    default: throw Error(DMX_E_INTERNAL, "bad epilogue");
+    if (epi == EPI_STATS) launch_x3_stats(bm, bn, sa, x1 ? 1 : 0, xp, grid, R.st);
+    else if (epi == EPI_BIAS || epi == EPI_BIAS_GELU || epi == EPI_BIAS_RES)
+      launch_x3_epi(epi, bm, bn, sa, x1 ? 1 : 0, xp, grid, R.st);
+    else throw Error(DMX_E_INTERNAL, "bad epilogue");
+  } else {
+    if (src_mode == SRC_NCHW && epi != EPI_STATS) throw Error(DMX_E_INTERNAL, "bad epilogue for NCHW source");
+    launch_f32(src_mode, epi, bm, bn, p, grid, R.st);
   }
   R.end();
   HIPCHK(hipGetLastError());
@@ -892,10 +743,7 @@ static void norm(Run& R, NormParams np, int N) {
   if (R.plan) return;
   // ~2048+ blocks in total, 256..1024 float4 per block (chunks are rounded up to 256 in-kernel)
   const int per = np.HW * (np.C / 4);
-  static const int target = [] {  // total blocks aimed at for small tensors
-    const char* e = std::getenv("DMX_NORM_BLOCKS");
-    return e ? std::atoi(e) : 1024;  // measured +0.3 % over 2048
-  }();
+  const int target = 1024;  // total blocks aimed at for small tensors (measured +0.3 % over 2048)
   const int chunks = std::max(1, std::min(cdiv(per, 256), std::max(cdiv(per, 1024), cdiv(target, N))));
   R.begin("norm_kernel", 0.0, 4.0 * (double)N * np.HW * np.C * (np.res ? 3 : 2));
   norm_kernel<<<dim3(chunks, N), 256, 0, R.st>>>(np);
@@ -1037,21 +885,13 @@ static void layernorm(Run& R, const float* x, float* y, const Vec& w, const Vec&
 static void attention_core(Run& R, const float* qkv, float* out, int N, int L, int C) {
   if (R.plan) return;
   const int D = C / 4;
+  if (D != 16 && D != 32 && D != 64) throw Error(DMX_E_INTERNAL, "attention: unsupported head dim");
   if (R.m->prec >= 1) {
     dim3 grid(cdiv(L, 128), 4, N);
-    static const int occ = [] {  // minimum waves per SIMD requested for D = 16 (register cap)
-      const char* e = std::getenv("DMX_ATT_OCC");
-      return e ? std::atoi(e) : 4;
-    }();
-    const int x1 = R.m->prec == 2 ? 1 : 0, wpe = (D == 16 && occ >= 4) ? 4 : 1;
+    const int x1 = R.m->prec == 2 ? 1 : 0, wpe = D == 16 ? 4 : 1;  // D = 16: >= 4 waves / SIMD (register cap)
     R.begin("attention_x3_kernel<" + std::to_string(D) + ", " + std::to_string(wpe) + ", " + std::to_string(x1) + ">",
             4.0 * N * (double)L * L * C, 4.0 * (double)N * L * 4 * C);
-#define ATX(DD, W, X) attention_x3_kernel<DD, W, X><<<grid, 256, 0, R.st>>>(qkv, out, L, C)
-    if (D == 16) { if (wpe == 4) { if (x1) ATX(16, 4, 1); else ATX(16, 4, 0); } else { if (x1) ATX(16, 1, 1); else ATX(16, 1, 0); } }
-    else if (D == 32) { if (x1) ATX(32, 1, 1); else ATX(32, 1, 0); }
-    else if (D == 64) { if (x1) ATX(64, 1, 1); else ATX(64, 1, 0); }
-    else throw Error(DMX_E_INTERNAL, "attention: unsupported head dim");
-#undef ATX
+    launch_attention_x3(D, wpe, x1, qkv, out, L, C, grid, R.st);
     R.end();
     HIPCHK(hipGetLastError());
     return;
@@ -1060,24 +900,20 @@ static void attention_core(Run& R, const float* qkv, float* out, int N, int L, i
   dim3 grid(cdiv(L, 64 * qt), 4, N);
   R.begin("attention_kernel<" + std::to_string(D) + ", " + std::to_string(qt) + ">", 4.0 * N * (double)L * L * C,
           4.0 * (double)N * L * 4 * C);
-#define ATT(DD, QQ) attention_kernel<DD, QQ><<<grid, 256, 0, R.st>>>(qkv, out, L, C)
-  if (D == 16) { if (qt == 2) ATT(16, 2); else ATT(16, 1); }
-  else if (D == 32) { if (qt == 2) ATT(32, 2); else ATT(32, 1); }
-  else if (D == 64) { if (qt == 2) ATT(64, 2); else ATT(64, 1); }
-  else throw Error(DMX_E_INTERNAL, "attention: unsupported head dim");
-#undef ATT
+  launch_attention_f32(D, qt, qkv, out, L, C, grid, R.st);
   R.end();
   HIPCHK(hipGetLastError());
 }
 
 static TokW tokw(const ConvW& c) { return TokW{c.Bh, c.Bl, c.bias, c.inv_scale, c.kpad}; }
 
-// Fused token kernels (tokmlp.h) for the x3 precision mode: TA -> attention core -> TB.
+// Fused token kernels (tokmlp.h) for the split-precision modes: TA -> attention core -> TB.
 static float* attn_block_fused(Run& R, const AttnW& a, const float* x, int N, int H, int W) {
   const int C = a.c, M = N * H * W, L = H * W;
   float* qkv = R.ws.get<float>((size_t)M * 3 * C);
   float* ao = R.ws.get<float>((size_t)M * C);
   float* out = R.ws.get<float>((size_t)M * C);
+  const int x1 = R.m->prec == 2 ? 1 : 0;
   if (!R.plan) {
     TokParams tp{};
     tp.x = x;
@@ -1089,63 +925,24 @@ static float* attn_block_fused(Run& R, const AttnW& a, const float* x, int N, in
     const std::string cs = std::to_string(C);
     tp.out = qkv;
     tp.w0 = tokw(a.qkv);
-    static const int nb64 = [] {  // C = 64: all 3C = 192 columns per block (LN1 + x read once)
-      const char* e = std::getenv("DMX_TOK_NB64");
-      return e ? std::atoi(e) : 192;
-    }();
-    static const int nb256 = [] {  // C = 256: 64 columns per block doubles the grid (M <= 8192 here)
-      const char* e = std::getenv("DMX_TOK_NB256");
-      return e ? std::atoi(e) : 64;
-    }();
-    static const bool lds_w = [] {  // weight slice resident in LDS, several token tiles per block
-      const char* e = std::getenv("DMX_TOK_LDS");
-      return e ? std::atoi(e) != 0 : true;
-    }();
-    const int x1 = R.m->prec == 2 ? 1 : 0;
-    if (lds_w && (C == 64 || C == 128)) {
+    if (C == 64 || C == 128) {
+      // in_proj slice resident in LDS, up to 4 token tiles per block; C = 64: all 3C = 192 columns per block
       const int nbl = C == 64 ? 192 : 64, gy = 3 * C / nbl, tiles = cdiv(M, 64);
       const int tpb = cdiv(tiles, 4) * gy >= 512 ? 4 : cdiv(tiles, 2) * gy >= 512 ? 2 : 1;
       const dim3 gl(cdiv(tiles, tpb), gy);
       R.begin("tok_ln_qkv_lds_kernel<" + cs + ", " + std::to_string(nbl) + ", " + std::to_string(tpb) + ", " +
                   std::to_string(x1) + ">",
               2.0 * M * C * 3.0 * C, 16.0 * (double)M * C);
-#define TQL(CC, NN, TT) (x1 ? tok_ln_qkv_lds_kernel<CC, NN, TT, 1><<<gl, 256, 0, R.st>>>(tp) \
-                            : tok_ln_qkv_lds_kernel<CC, NN, TT, 0><<<gl, 256, 0, R.st>>>(tp))
-      if (C == 64) {
-        if (tpb == 4) TQL(64, 192, 4);
-        else if (tpb == 2) TQL(64, 192, 2);
-        else TQL(64, 192, 1);
-      } else {
-        if (tpb == 4) TQL(128, 64, 4);
-        else if (tpb == 2) TQL(128, 64, 2);
-        else TQL(128, 64, 1);
-      }
-#undef TQL
-      R.end();
-      HIPCHK(hipGetLastError());
+      launch_tok_qkv_lds(C, tpb, x1, tp, gl, R.st);
+    } else {
+      const int nb = 64;  // C = 256: 64 columns per block doubles the grid (M <= 8192 here)
+      const dim3 grid(cdiv(M, 64), 3 * C / nb);
+      R.begin("tok_ln_qkv_kernel<" + cs + ", " + std::to_string(nb) + ", " + std::to_string(x1) + ">",
+              2.0 * M * C * 3.0 * C, 16.0 * (double)M * C);
+      launch_tok_qkv(C, nb, x1, tp, grid, R.st);
     }
-    const int nb = C == 64 ? nb64 : C == 256 ? nb256 : 128;  // output columns per block (grid.y = 3C / nb)
-    const dim3 grid(cdiv(M, 64), 3 * C / nb);
-    if (!(lds_w && (C == 64 || C == 128))) {
-    R.begin("tok_ln_qkv_kernel<" + cs + ", " + std::to_string(nb) + ", " + std::to_string(x1) + ">",
-            2.0 * M * C * 3.0 * C, 16.0 * (double)M * C);
-#define TQ(CC, NN) (x1 ? tok_ln_qkv_kernel<CC, NN, 1><<<grid, 256, 0, R.st>>>(tp) \
-                       : tok_ln_qkv_kernel<CC, NN, 0><<<grid, 256, 0, R.st>>>(tp))
-    switch (C) {
-      case 64:
-        if (nb == 192) TQ(64, 192);
-        else TQ(64, 64);
-        break;
-      case 128: TQ(128, 128); break;
-      default:
-        if (nb == 64) TQ(256, 64);
-        else TQ(256, 128);
-        break;
-    }
-#undef TQ
     R.end();
     HIPCHK(hipGetLastError());
-    }
   }
   attention_core(R, qkv, ao, N, L, C);
   if (!R.plan) {
@@ -1163,42 +960,15 @@ static float* attn_block_fused(Run& R, const AttnW& a, const float* x, int N, in
     tp.w2 = tokw(a.f2);
     // 32-token tiles when 64-token tiles would leave the chip under-filled (or C = 256)
     const int tm = C == 64 ? 64 : (C == 256 || cdiv(M, 64) < 512) ? 32 : 64;
-    const int blocks = cdiv(M, tm);
-    const int x1 = R.m->prec == 2 ? 1 : 0;
-    static const int nw256 = [] {  // C = 256: 8 waves per 32-token tile (one 32-column tile each)
-      const char* e = std::getenv("DMX_TOK_NW256");
-      return e ? std::atoi(e) : 8;
-    }();
-    static const bool tb_lds = [] {  // C = 64: weights in LDS, 128-token tiles, 8 waves, several tiles / block
-      const char* e = std::getenv("DMX_TOKB_LDS");
-      return e ? std::atoi(e) != 0 : true;
-    }();
-    const bool lds64 = tb_lds && C == 64;
+    const bool lds64 = C == 64;  // weights in LDS, 128-token tiles, 8 waves, several tiles / block
     const int tiles128 = cdiv(M, 128), tpb = lds64 ? (tiles128 >= 1024 ? 4 : tiles128 >= 512 ? 2 : 1) : 1;
-    const int nw = C == 256 ? nw256 : lds64 ? 8 : 4;
+    const int nw = C == 256 ? 8 : lds64 ? 8 : 4;
     const int tmk = lds64 ? 128 : tm;
+    const int blocks = lds64 ? cdiv(tiles128, tpb) : cdiv(M, tm);
     R.begin("tok_attn_out_kernel<" + std::to_string(C) + ", " + std::to_string(tmk) + ", " + std::to_string(x1) +
                 ", " + std::to_string(nw) + ", " + std::to_string(lds64 ? 1 : 0) + ", " + std::to_string(tpb) + ">",
-            6.0 * M * (double)C * C,
-            12.0 * (double)M * C);
-#define TB(CC, TT) (x1 ? tok_attn_out_kernel<CC, TT, 1><<<blocks, 256, 0, R.st>>>(tp) \
-                       : tok_attn_out_kernel<CC, TT, 0><<<blocks, 256, 0, R.st>>>(tp))
-    if (lds64) {
-      const int bl = cdiv(tiles128, tpb);
-#define TBL(TP) (x1 ? tok_attn_out_kernel<64, 128, 1, 8, 1, TP><<<bl, 512, 0, R.st>>>(tp) \
-                    : tok_attn_out_kernel<64, 128, 0, 8, 1, TP><<<bl, 512, 0, R.st>>>(tp))
-      if (tpb == 4) TBL(4);
-      else if (tpb == 2) TBL(2);
-      else TBL(1);
-#undef TBL
-    } else if (C == 64) TB(64, 64);
-    else if (C == 128 && tm == 64) TB(128, 64);
-    else if (C == 128) TB(128, 32);
-    else if (nw == 8) {
-      if (x1) tok_attn_out_kernel<256, 32, 1, 8><<<blocks, 512, 0, R.st>>>(tp);
-      else tok_attn_out_kernel<256, 32, 0, 8><<<blocks, 512, 0, R.st>>>(tp);
-    } else TB(256, 32);
-#undef TB
+            6.0 * M * (double)C * C, 12.0 * (double)M * C);
+    launch_tok_out(C, tm, x1, nw, lds64 ? 1 : 0, tpb, tp, blocks, R.st);
     R.end();
     HIPCHK(hipGetLastError());
   }
@@ -1208,18 +978,10 @@ static float* attn_block_fused(Run& R, const AttnW& a, const float* x, int N, in
   return out;
 }
 
-static bool tok_fused_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("DMX_TOK_FUSED");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 // AttenionBlock (models/unet_cond.py:32-52) on NHWC == (N, L, C) tokens.
 static float* attn_block(Run& R, const AttnW& a, const float* x, int N, int H, int W) {
   const int C = a.c, M = N * H * W, L = H * W;
-  if (R.m->prec >= 1 && tok_fused_enabled() && (C == 64 || C == 128 || C == 256) && a.qkv.kpad == C &&
+  if (R.m->prec >= 1 && (C == 64 || C == 128 || C == 256) && a.qkv.kpad == C &&
       a.o.kpad == C && a.f1.kpad == C && a.f2.kpad == C)
     return attn_block_fused(R, a, x, N, H, W);
   float* xl = R.ws.get<float>((size_t)M * C);
@@ -1273,7 +1035,7 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
     e.cond_rows = in.cond_rows > 0 ? in.cond_rows : N;
     e.pos_table = m->ctx->pos_table;
     e.class_emb = m->class_emb;
-    e.ncls = 4;
+    e.ncls = m->cfg.ncls;
     e.w0 = m->w0;
     e.b0 = m->b0;
     e.w2t = m->w2t;
@@ -1443,6 +1205,7 @@ static void step_body(Run& R, const dmx_step_args& a) {
   p.noise = a.noise;
   p.seed = a.seed;
   p.sample_offset = a.sample_offset;
+  p.range_flag = m->range_flag;
   R.layer = "out+cfg+ddpm";
   if (p.Co == 4 && p.feat != nullptr) {
     dim3 grid(cdiv(p.HW, 16), a.n);
@@ -1476,7 +1239,7 @@ static void vae_body(Run& R, const float* z, float* img, uint8_t* u8, int n, int
   const int G = 8;
   SrcDesc s = plain_src(z, 4);
   s.C0 = 4;
-  s.scale = 0.18215f;
+  s.scale = m->cfg.scale;
   int mode = SRC_NCHW;
   int H = h, W = w;
   const float* act = nullptr;
@@ -1507,7 +1270,7 @@ static void vae_body(Run& R, const float* z, float* img, uint8_t* u8, int n, int
   if (R.plan) return;
   dim3 grid(cdiv(H * W, 256), n);
   R.begin("vae_tail_kernel", 2.0 * n * H * W * 3 * 576, 4.0 * (double)n * H * W * (64 + 3) + (double)n * H * W * 3);
-  vae_tail_kernel<<<grid, 256, 0, R.st>>>(act, m->vconv[3].B, m->vconv[3].bias, n, H, W, img, u8);
+  vae_tail_kernel<<<grid, 256, 0, R.st>>>(act, m->vconv[3].B, m->vconv[3].bias, n, H, W, img, u8, m->range_flag);
   R.end();
   HIPCHK(hipGetLastError());
 }
@@ -1550,8 +1313,8 @@ static void vae_enc_body(Run& R, const float* x, const float* eps, float* z, flo
   }
   if (R.plan) return;
   R.begin("vae_enc_tail_kernel", 2.0 * n * H * W * 8 * 256, 4.0 * (double)n * H * W * (256 + 4 + 4));
-  vae_enc_tail_kernel<<<n, 256, 0, R.st>>>(act, m->wmu, m->bmu, m->wlv, m->blv, eps, z, kl, H * W, 0.18215f,
-                                            1.0f / ((float)h * (float)w));
+  vae_enc_tail_kernel<<<n, 256, 0, R.st>>>(act, m->wmu, m->bmu, m->wlv, m->blv, eps, z, kl, H * W, m->cfg.scale,
+                                            1.0f / ((float)h * (float)w), m->range_flag);
   R.end();
   HIPCHK(hipGetLastError());
 }
@@ -1578,6 +1341,36 @@ static int guarded(F&& f) {
     g_err = "unknown error";
     return DMX_E_INTERNAL;
   }
+}
+
+static ModelCfg to_cfg(const dmx_model_config& c) {
+  ModelCfg m;
+  REQUIRE(c.kind >= DMX_UNET_COND_GEOM && c.kind <= DMX_VAE, "unknown model kind");
+  REQUIRE(c.in_ch >= 1 && c.in_ch <= 4, "in_ch must be in [1,4]");
+  REQUIRE(c.num_classes >= 0 && c.num_classes < (1 << 20), "bad num_classes");
+  REQUIRE(c.geom_dim >= 1 && c.geom_dim <= 4096 && c.geom_hidden >= 1 && c.geom_hidden <= 4096,
+          "geom_dim / geom_hidden must be in [1, 4096]");
+  REQUIRE(std::isfinite(c.scale_factor) && c.scale_factor != 0.f, "scale_factor must be finite and non-zero");
+  m.kind = c.kind;
+  m.in_ch = c.in_ch;
+  m.deep = !c.remove_deep_conv;
+  m.ncls = c.num_classes + 1;
+  m.gdim = c.geom_dim;
+  m.ghid = c.geom_hidden;
+  m.scale = c.scale_factor;
+  return m;
+}
+
+static dmx_model_config default_cfg(int kind, int in_ch, int remove_deep_conv) {
+  dmx_model_config c;
+  c.kind = kind;
+  c.in_ch = in_ch;
+  c.remove_deep_conv = remove_deep_conv;
+  c.num_classes = 3;
+  c.geom_dim = 12;
+  c.geom_hidden = 256;
+  c.scale_factor = 0.18215f;
+  return c;
 }
 
 extern "C" {
@@ -1611,18 +1404,33 @@ int dmx_set_time_table(dmx_ctx* ctx, const float* host_table, int tmax) {
     HIPCHK(hipMalloc(&ctx->pos_table, (size_t)tmax * 256 * sizeof(float)));
     HIPCHK(hipMemcpy(ctx->pos_table, host_table, (size_t)tmax * 256 * sizeof(float), hipMemcpyHostToDevice));
     ctx->tmax = tmax;
+    ++ctx->table_gen;
   });
 }
 
+int dmx_model_cfg_num_keys(const dmx_model_config* cfg) {
+  if (cfg == nullptr) return -1;
+  int n = -1;
+  if (guarded([&] { n = (int)model_keys(to_cfg(*cfg)).size(); }) != DMX_OK) return -1;
+  return n;
+}
+
 int dmx_model_num_keys(int kind, int in_ch, int remove_deep_conv) {
-  if (kind < DMX_UNET_COND_GEOM || kind > DMX_VAE) return -1;
-  return (int)model_keys(kind, in_ch, !remove_deep_conv).size();
+  const dmx_model_config c = default_cfg(kind, in_ch, remove_deep_conv);
+  return dmx_model_cfg_num_keys(&c);
 }
 
 int dmx_model_key(int kind, int in_ch, int remove_deep_conv, int index, char* name_out, int name_cap,
                   int64_t* shape_out, int* ndim_out) {
+  const dmx_model_config c = default_cfg(kind, in_ch, remove_deep_conv);
+  return dmx_model_cfg_key(&c, index, name_out, name_cap, shape_out, ndim_out);
+}
+
+int dmx_model_cfg_key(const dmx_model_config* cfg, int index, char* name_out, int name_cap, int64_t* shape_out,
+                      int* ndim_out) {
   return guarded([&] {
-    Keys k = model_keys(kind, in_ch, !remove_deep_conv);
+    REQUIRE(cfg != nullptr, "null config");
+    Keys k = model_keys(to_cfg(*cfg));
     REQUIRE(index >= 0 && index < (int)k.size(), "key index out of range");
     REQUIRE(name_out && name_cap > (int)k[index].name.size(), "name buffer too small");
     std::strcpy(name_out, k[index].name.c_str());
@@ -1632,19 +1440,24 @@ int dmx_model_key(int kind, int in_ch, int remove_deep_conv, int index, char* na
   });
 }
 
-int dmx_model_create(dmx_ctx* ctx, int kind, int in_ch, int remove_deep_conv, dmx_model** out) {
+int dmx_model_create_cfg(dmx_ctx* ctx, const dmx_model_config* cfg, dmx_model** out) {
   return guarded([&] {
-    REQUIRE(ctx && out, "null argument");
-    REQUIRE(kind >= DMX_UNET_COND_GEOM && kind <= DMX_VAE, "unknown model kind");
-    REQUIRE(in_ch >= 1 && in_ch <= 4, "in_ch must be in [1,4]");
+    REQUIRE(ctx && cfg && out, "null argument");
+    const ModelCfg c = to_cfg(*cfg);
     auto* m = new dmx_model();
     m->ctx = ctx;
-    m->kind = kind;
-    m->in_ch = in_ch;
-    m->deep = !remove_deep_conv;
-    m->keys = model_keys(kind, in_ch, m->deep);
+    m->cfg = c;
+    m->kind = c.kind;
+    m->in_ch = c.in_ch;
+    m->deep = c.deep;
+    m->keys = model_keys(c);
     *out = m;
   });
+}
+
+int dmx_model_create(dmx_ctx* ctx, int kind, int in_ch, int remove_deep_conv, dmx_model** out) {
+  const dmx_model_config c = default_cfg(kind, in_ch, remove_deep_conv);
+  return dmx_model_create_cfg(ctx, &c, out);
 }
 
 int dmx_model_destroy(dmx_model* m) {
@@ -1700,6 +1513,19 @@ int dmx_model_set_precision(dmx_model* m, int prec) {
 
 int dmx_model_get_precision(const dmx_model* m) { return m ? m->prec : -1; }
 
+int dmx_model_range_check(dmx_model* m, int reset, int* flagged, void* stream) {
+  return guarded([&] {
+    REQUIRE(m != nullptr && flagged != nullptr, "null argument");
+    if (!m->finalized) throw Error(DMX_E_STATE, "model weights not finalized");
+    hipStream_t st = (hipStream_t)stream;
+    int v = 0;
+    HIPCHK(hipMemcpyAsync(&v, m->range_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    *flagged = v;
+    if (reset) HIPCHK(hipMemsetAsync(m->range_flag, 0, sizeof(int), st));
+  });
+}
+
 int dmx_debug_enable(dmx_model* m, int on) {
   return guarded([&] {
     REQUIRE(m != nullptr, "null model");
@@ -1739,10 +1565,11 @@ int dmx_unet_forward(dmx_model* m, const float* x, const int64_t* t, const int64
       float* feat = unet_trunk(R, in, n, h, w);
       if (R.plan) return;
       dim3 grid(cdiv(h * w, 256), n);
-      out_head_kernel<<<grid, 256, 0, st>>>(feat, m->out_w, m->out_b, eps, m->in_ch, h * w);
+      out_head_kernel<<<grid, 256, 0, st>>>(feat, m->out_w, m->out_b, eps, m->in_ch, h * w, m->range_flag);
       HIPCHK(hipGetLastError());
       if (geom) {
-        geom_head_kernel<<<n, 256, 0, st>>>(feat, h * w, m->gw0, m->gb0, m->gw2, m->gb2, 12, geom);
+        geom_head_kernel<<<n, 256, (64 + m->cfg.ghid) * sizeof(float), st>>>(feat, h * w, m->gw0, m->gb0, m->gw2, m->gb2,
+                                                                             m->cfg.ghid, m->cfg.gdim, geom);
         HIPCHK(hipGetLastError());
       }
     });
@@ -1778,6 +1605,7 @@ int dmx_sample_loop(dmx_model* m, const dmx_step_args* a, int steps, int use_gra
     GraphKey key;
     std::memset(&key, 0, sizeof(key));
     std::memcpy(&key.a, a, sizeof(dmx_step_args));
+    key.table_gen = m->ctx->table_gen;
     if (!(m->has_graph && key == m->gkey)) {
       if (m->has_graph) {
         (void)hipGraphExecDestroy(m->gexec);
@@ -1903,6 +1731,15 @@ int dmx_vae_decode(dmx_model* m, const float* z, float* img, uint8_t* u8, int n,
                  u8 ? u8 + (size_t)s * 64 * h * w * 3 : nullptr, b, h, w);
       });
     }
+  });
+}
+
+int dmx_latent_frames_u8(const float* z, uint8_t* out, int n, int c, int h, int w, void* stream) {
+  return guarded([&] {
+    REQUIRE(z && out, "null tensor");
+    REQUIRE(n >= 1 && c >= 1 && h >= 1 && w >= 1, "bad shape");
+    latent_frames_kernel<<<n * c, 256, 0, (hipStream_t)stream>>>(z, out, h * w);
+    HIPCHK(hipGetLastError());
   });
 }
 

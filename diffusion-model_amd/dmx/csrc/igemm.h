@@ -397,7 +397,7 @@ struct SplitkParams {
   const float* bias; const float* res; float* out; float2* rowpart; int seg; int epi;
 };
 
-__global__ __launch_bounds__(256) void splitk_reduce_kernel(const SplitkParams p) {
+static __global__ __launch_bounds__(256) void splitk_reduce_kernel(const SplitkParams p) {
   const int C4 = p.Cout / 4;
   const size_t total = (size_t)p.M * C4;
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;

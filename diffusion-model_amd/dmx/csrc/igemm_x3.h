@@ -20,7 +20,7 @@ namespace dmx {
 
 
 // 16 readable zero bytes: the load target of masked (padding) A pieces.
-__device__ __attribute__((aligned(16))) float g_zero16[4] = {0.f, 0.f, 0.f, 0.f};
+static __device__ __attribute__((aligned(16))) float g_zero16[4] = {0.f, 0.f, 0.f, 0.f};
 
 constexpr int X3_BK = 32;
 constexpr int X3_STRIDE = 40;  // f16 per LDS row (32 + 8 pad) = 80 bytes
@@ -271,183 +271,7 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
   igemm_epilogue<BM, BN, EPI>(p, acc, phase, m0, n0, wm, wn, fr, fh);
 }
 
-// ---------------------------------------------------------------------------
-// x3 implicit GEMM, LDS-DMA pipeline (A = fp16 hi/lo activation planes).
-//
-// Both operands go global -> LDS with global_load_lds_dwordx4 (no VGPR round trip, no
-// ds_write): the next K-tile's DMA is issued into the other buffer before the current
-// tile's ds_read + MFMA, and one vmcnt(0) + barrier per K-tile retires it
-// (cdna_hip_programming.md §5.5 T3+T4, "minimum 2-phase").  BK = 32: an operand row is
-// 64 B (4 chunks of 16 B) per plane; one DMA instruction fills 16 rows x 4 chunks = 1 KiB
-// lane-linearly, so the bank swizzle lives on the SOURCE side: LDS slot j of row r holds
-// k-chunk j ^ ((r >> 2) & 3), and a fragment read of chunk c goes to slot c ^ ((r >> 2) & 3)
-// — the 16 rows of every ds_read_b128 lane group land on 16 distinct 16-B slots.
-// Padding taps / rows past M / k past Kreal read the zero page (address select).
-// ---------------------------------------------------------------------------
-// s_waitcnt vmcnt(N) lgkmcnt(0) (expcnt left at "no wait"), gfx9 encoding: vmcnt bits
-// [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8].
-template <int N>
-DMX_DEV void wait_vm_lgkm0() {
-  static_assert(N >= 0 && N < 64, "vmcnt");
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4));
-}
-
-template <int BM, int BN, int EPI, int NST = 2>
-__global__ __launch_bounds__(256) void igemm_x3g_kernel(const X3Params P) {
-  const IgemmParams& p = P.g;
-  constexpr int BK = 32, ROWB = 64;                       // bytes per operand row per plane
-  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
-  constexpr int AQ = BM / 64, BQ = BN / 64;               // 16-row DMA pieces per wave (A, B)
-  constexpr int PLA = BM * ROWB, PLB = BN * ROWB;         // bytes per plane
-  constexpr int BUF = 2 * PLA + 2 * PLB;                  // Ah | Al | Bh | Bl
-  static_assert(TM >= 1 && TN >= 1 && AQ >= 1 && BQ >= 1, "tile");
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[NST * BUF];
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  int mt, nt, bz;
-  xcd_tile(mt, nt, bz);
-  const int phase = EPI == EPI_PARTIAL ? 0 : bz;
-  const int m0 = mt * BM, n0 = nt * BN;
-  const size_t boff = (size_t)phase * p.Npad * p.Kpad;
-  const _Float16* Bh = P.Bh + boff;
-  const _Float16* Bl = P.Bl + boff;
-  const int HW = p.H * p.W, C = p.src.C;
-
-  // This lane's DMA rows: A rows wid*(BM/4) + 16q + lane/4, B rows wid*(BN/4) + 16q + lane/4;
-  // it loads k-chunk (lane & 3) ^ ((row >> 2) & 3) of each.
-  const int lr = lane >> 2, lj = lane & 3;
-  int rpix[AQ], achunk[AQ];
-  unsigned tmask[AQ];
-#pragma unroll
-  for (int q = 0; q < AQ; ++q) {
-    const int row = wid * (BM / 4) + 16 * q + lr;
-    achunk[q] = lj ^ ((row >> 2) & 3);
-    const int m = m0 + row;
-    rpix[q] = m < p.M ? row_anchor(p.geom, m, p.H, p.W, p.Hin, p.Win) : 0;
-    tmask[q] = tap_mask(p.geom, phase, p.taps, m, p.M, p.H, p.W, p.Hin, p.Win);
-  }
-  size_t brow[BQ];  // element offset of this lane's B chunk in the [Npad][Kpad] planes (k-tile 0)
-#pragma unroll
-  for (int q = 0; q < BQ; ++q) {
-    const int row = wid * (BN / 4) + 16 * q + lr;
-    brow[q] = (size_t)(n0 + row) * p.Kpad + 8 * (lj ^ ((row >> 2) & 3));
-  }
-  typedef __attribute__((address_space(1))) void gvoid;
-  typedef __attribute__((address_space(3))) void lvoid;
-  auto dma = [&](const void* g, unsigned char* l) {
-    __builtin_amdgcn_global_load_lds((gvoid*)g, (lvoid*)l, 16, 0, 0);
-  };
-  auto stage = [&](int kt, int buf) {
-    unsigned char* L = lds + buf * BUF;
-#pragma unroll
-    for (int q = 0; q < AQ; ++q) {
-      const int k = kt * BK + 8 * achunk[q];
-      const int tap = k / C, c = k - tap * C;
-      int dy, dx;
-      tap_offset(p.geom, phase, tap, dy, dx);
-      const bool ok = tap < 32 && ((tmask[q] >> tap) & 1u);
-      const int off = (rpix[q] + dy * p.Win + dx) * C + c;
-      const void* gh = ok ? (const void*)(P.Ash + off) : (const void*)g_zero16;
-      const void* gl = ok ? (const void*)(P.Asl + off) : (const void*)g_zero16;
-      const int rb = (wid * (BM / 4) + 16 * q) * ROWB;
-      dma(gh, L + rb);
-      dma(gl, L + PLA + rb);
-    }
-#pragma unroll
-    for (int q = 0; q < BQ; ++q) {
-      const size_t o = brow[q] + kt * BK;
-      const int rb = (wid * (BN / 4) + 16 * q) * ROWB;
-      dma(Bh + o, L + 2 * PLA + rb);
-      dma(Bl + o, L + 2 * PLA + PLB + rb);
-    }
-  };
-
-  floatx16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int fr = lane & 31, fh = lane >> 5;
-  auto compute = [&](int buf) {
-    const unsigned char* L = lds + buf * BUF;
-#pragma unroll
-    for (int s = 0; s < BK / 16; ++s) {
-      const int cidx = 2 * s + fh;
-      half8 ah[TM], al[TM], bh[TN], bl[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * WM + i * 32 + fr;
-        const int o = row * ROWB + 16 * (cidx ^ ((row >> 2) & 3));
-        ah[i] = *reinterpret_cast<const half8*>(L + o);
-        al[i] = *reinterpret_cast<const half8*>(L + PLA + o);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = wn * WN + j * 32 + fr;
-        const int o = row * ROWB + 16 * (cidx ^ ((row >> 2) & 3));
-        bh[j] = *reinterpret_cast<const half8*>(L + 2 * PLA + o);
-        bl[j] = *reinterpret_cast<const half8*>(L + 2 * PLA + PLB + o);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-        }
-    }
-  };
-
-  int kbeg = 0, nK = p.Kpad / BK;
-  if constexpr (EPI == EPI_PARTIAL) {
-    kbeg = blockIdx.z * p.ksplit;
-    nK = min(nK - kbeg, p.ksplit);
-  }
-  if constexpr (NST == 2) {
-    stage(kbeg, 0);
-    __syncthreads();  // vmcnt(0) + barrier: tile 0 resident
-    for (int t = 0; t < nK; ++t) {
-      const int buf = t & 1;
-      if (t + 1 < nK) stage(kbeg + t + 1, buf ^ 1);  // DMA in flight during this tile's MFMAs
-      compute(buf);
-      __syncthreads();  // retires the DMA (vmcnt(0)) and every wave's reads of `buf`
-    }
-  } else {
-    // 3 buffers, one tile in flight across each barrier: at iteration t this wave waits
-    // until only tile t+1's DMA (G instructions) is outstanding, the raw barrier makes every
-    // wave's tile-t DMA visible and retires every wave's reads of tile t-1's buffer, which
-    // is then restaged with tile t+2.
-    constexpr int G = 2 * (AQ + BQ);  // DMA instructions per wave per tile
-    stage(kbeg, 0);
-    if (nK > 1) stage(kbeg + 1, 1);
-    int buf = 0;
-    for (int t = 0; t < nK; ++t) {
-      // this wave: tile t landed, its ds_reads of tile t-1 returned; then the raw barrier
-      if (t + 1 < nK) wait_vm_lgkm0<G>();
-      else wait_vm_lgkm0<0>();
-      __builtin_amdgcn_s_barrier();
-      if (t + 2 < nK) stage(kbeg + t + 2, buf == 0 ? 2 : buf - 1);
-      compute(buf);
-      buf = buf == 2 ? 0 : buf + 1;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] *= P.inv_scale;
-
-  igemm_epilogue<BM, BN, EPI>(p, acc, phase, m0, n0, wm, wn, fr, fh);
-}
-
-// Split fp32 weights (already in the B layout) into scaled f16 hi / lo planes.
-__global__ void split_weights_kernel(const float* src, _Float16* hi, _Float16* lo, size_t n, float scale) {
+static __global__ void split_weights_kernel(const float* src, _Float16* hi, _Float16* lo, size_t n, float scale) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     const float v = src[i] * scale;
     const _Float16 h = (_Float16)v;
@@ -456,7 +280,7 @@ __global__ void split_weights_kernel(const float* src, _Float16* hi, _Float16* l
   }
 }
 
-__global__ void absmax_kernel(const float* src, size_t n, unsigned* out) {
+static __global__ void absmax_kernel(const float* src, size_t n, unsigned* out) {
   float m = 0.f;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
     m = fmaxf(m, fabsf(src[i]));

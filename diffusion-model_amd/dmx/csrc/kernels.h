@@ -42,7 +42,7 @@ struct EmbedParams {
 
 // grid = (n, parts): every block recomputes the sample's 256-wide embedding (cheap) and
 // produces its 1/parts slice of the concatenated head outputs (coalesced weight reads).
-__global__ __launch_bounds__(256) void embed_kernel(const EmbedParams p) {
+static __global__ __launch_bounds__(256) void embed_kernel(const EmbedParams p) {
   __shared__ float s[256], h[256], in24[24];
   const int n = blockIdx.x, k = threadIdx.x;
   int64_t t = p.t[(size_t)(p.t_mod ? n % p.t_mod : n) * p.t_stride];
@@ -99,7 +99,7 @@ __global__ __launch_bounds__(256) void embed_kernel(const EmbedParams p) {
 // ---------------------------------------------------------------------------
 // rowpart layout: [n][R rows][nseg] (R = partial rows per sample); elements per
 // group = HWo * C / G.
-__global__ __launch_bounds__(256) void gn_finalize_kernel(const float2* rowpart, float2* stats, int R, int nseg,
+static __global__ __launch_bounds__(256) void gn_finalize_kernel(const float2* rowpart, float2* stats, int R, int nseg,
                                                            int G, int C, int HWo, float eps) {
   const int ng = blockIdx.x, n = ng / G, g = ng % G;
   const int spg = nseg / G;
@@ -154,7 +154,7 @@ struct NormParams {
   _Float16* out_h; _Float16* out_l;  // optional fp16 hi/lo planes (split-precision GEMM operand)
 };
 
-__global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
+static __global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
   const int n = blockIdx.y, tid = threadIdx.x;
   const int ns = p.n_src > 0 ? n % p.n_src : n;  // source sample (CFG-shared trunk prefix)
   // This block's float4 range [beg, end) of the sample; chunks are multiples of 256, so when
@@ -604,7 +604,16 @@ struct StepTailParams {
   const float* c1; const float* c2; const float* sd;  // [tmax], index t-1
   const float* noise;                                 // NCHW or null => Philox
   uint64_t seed; int64_t sample_offset;
+  int* range_flag;                                    // set to 1 when eps is not finite (or null)
 };
+
+// Range guard of the split-precision modes: an operand beyond the f16 range (|v| >= 65520)
+// becomes inf in its hi plane, and any inf / NaN reaching a network output makes that output
+// non-finite.  Output kernels raise a sticky flag (a plain vector store) that the host reads
+// at its checkpoints and answers by recomputing in exact-fp32 MFMA mode.
+DMX_DEV void flag_nonfinite(int* flag, float v) {
+  if (flag != nullptr && !(fabsf(v) <= 3.402823466e38f)) *flag = 1;
+}
 
 // One IEEE rounding per reference op: the product is forced through a register
 // (opaque asm barrier) so no multiply-add pair can be contracted into an FMA,
@@ -618,7 +627,7 @@ DMX_DEV float ddpm_elem(float x, float eps, float c1, float c2, float sd, float 
   return mu + rnd(nz * sd);
 }
 
-__global__ __launch_bounds__(256) void step_tail_kernel(const StepTailParams p) {
+static __global__ __launch_bounds__(256) void step_tail_kernel(const StepTailParams p) {
   const int pix = blockIdx.x * 256 + threadIdx.x;
   const int n = blockIdx.y;
   if (pix >= p.HW) return;
@@ -664,6 +673,7 @@ __global__ __launch_bounds__(256) void step_tail_kernel(const StepTailParams p) 
   const float c1 = p.c1[t - 1], c2 = p.c2[t - 1], sd = p.sd[t - 1];
   for (int c = 0; c < Co; ++c) {
     const float eps = p.cfg ? eu[c] + rnd(p.guidance * rnd(ec[c] - eu[c])) : eu[c];
+    flag_nonfinite(p.range_flag, eps);
     const size_t idx = ((size_t)n * Co + c) * p.HW + pix;
     p.x_out[idx] = ddpm_elem(p.x[idx], eps, c1, c2, sd, nz[c]);
   }
@@ -686,7 +696,7 @@ DMX_DEV float group_sum16(float s) {  // sum over aligned 16-lane rows (DPP), sa
   return s;
 }
 
-__global__ __launch_bounds__(256) void step_tail4_kernel(const StepTailParams p) {
+static __global__ __launch_bounds__(256) void step_tail4_kernel(const StepTailParams p) {
   const int sub = threadIdx.x & 15, pix = blockIdx.x * 16 + (threadIdx.x >> 4), n = blockIdx.y;
   const bool valid = pix < p.HW;
   const int pc = valid ? pix : 0;
@@ -723,12 +733,13 @@ __global__ __launch_bounds__(256) void step_tail4_kernel(const StepTailParams p)
     }
   }
   const float eps = p.cfg ? u + rnd(p.guidance * rnd(v - u)) : u;
+  flag_nonfinite(p.range_flag, eps);
   p.x_out[idx] = ddpm_elem(p.x[idx], eps, p.c1[t - 1], p.c2[t - 1], p.sd[t - 1], nz);
 }
 
 // conv1x1 64 -> Co + bias into NCHW (models/unet_cond.py:153, the `out` layer).
-__global__ __launch_bounds__(256) void out_head_kernel(const float* feat, const float* w, const float* b, float* eps,
-                                                       int Co, int HW) {
+static __global__ __launch_bounds__(256) void out_head_kernel(const float* feat, const float* w, const float* b, float* eps,
+                                                       int Co, int HW, int* range_flag) {
   const int pix = blockIdx.x * 256 + threadIdx.x, n = blockIdx.y;
   if (pix >= HW) return;
   const float* f = feat + ((size_t)n * HW + pix) * 64;
@@ -742,14 +753,21 @@ __global__ __launch_bounds__(256) void out_head_kernel(const float* feat, const 
       for (int j = 0; j < 4; ++j) acc[c] += ww[j] * a[j];
     }
   }
-  for (int c = 0; c < Co; ++c) eps[((size_t)n * Co + c) * HW + pix] = acc[c];
+  for (int c = 0; c < Co; ++c) {
+    flag_nonfinite(range_flag, acc[c]);
+    eps[((size_t)n * Co + c) * HW + pix] = acc[c];
+  }
 }
 
-// GeomHead: GAP over HW of feat (64 ch) -> Linear(64->256) -> SiLU -> Linear(256->12)
-// (models/unet_cond_geom.py:8-23).  One block per sample.
-__global__ __launch_bounds__(256) void geom_head_kernel(const float* feat, int HW, const float* w0, const float* b0,
-                                                        const float* w2, const float* b2, int gdim, float* geom) {
-  __shared__ float part[4][64], g[64], h[256];
+// GeomHead: GAP over HW of feat (64 ch) -> Linear(64->hid) -> SiLU -> Linear(hid->gdim)
+// (models/unet_cond_geom.py:8-23).  One block per sample; dynamic LDS = (64 + hid) floats.
+static __global__ __launch_bounds__(256) void geom_head_kernel(const float* feat, int HW, const float* w0, const float* b0,
+                                                        const float* w2, const float* b2, int hid, int gdim,
+                                                        float* geom) {
+  extern __shared__ float sm[];
+  __shared__ float part[4][64];
+  float* g = sm;
+  float* h = sm + 64;
   const int n = blockIdx.x, tid = threadIdx.x, c = tid & 63, sl = tid >> 6;
   float s = 0.f;
   for (int pix = sl; pix < HW; pix += 4) s += feat[((size_t)n * HW + pix) * 64 + c];
@@ -757,22 +775,24 @@ __global__ __launch_bounds__(256) void geom_head_kernel(const float* feat, int H
   __syncthreads();
   if (tid < 64) g[tid] = (part[0][tid] + part[1][tid] + part[2][tid] + part[3][tid]) / (float)HW;
   __syncthreads();
-  float a = b0[tid];
-  for (int k = 0; k < 64; ++k) a += w0[tid * 64 + k] * g[k];
-  h[tid] = silu(a);
+  for (int j = tid; j < hid; j += 256) {
+    float a = b0[j];
+    for (int k = 0; k < 64; ++k) a += w0[j * 64 + k] * g[k];
+    h[j] = silu(a);
+  }
   __syncthreads();
-  if (tid < gdim) {
-    float o = b2[tid];
-    for (int k = 0; k < 256; ++k) o += w2[tid * 256 + k] * h[k];
-    geom[n * gdim + tid] = o;
+  for (int o = tid; o < gdim; o += 256) {
+    float acc = b2[o];
+    for (int k = 0; k < hid; ++k) acc += w2[(size_t)o * hid + k] * h[k];
+    geom[(size_t)n * gdim + o] = acc;
   }
 }
 
 // VAE tail: conv3x3 64->3 + bias (dec.18) -> sigmoid (models/vae.py:49,69), then
 // diff.py:58-62's x*255 -> clamp(0,255) -> uint8 (truncation), HWC for PIL.
 // in: materialised GELU(GN(dec.15)) NHWC [N][H][W][64].
-__global__ __launch_bounds__(256) void vae_tail_kernel(const float* in, const float* w, const float* b, int N, int H,
-                                                       int W, float* img, uint8_t* u8) {
+static __global__ __launch_bounds__(256) void vae_tail_kernel(const float* in, const float* w, const float* b, int N, int H,
+                                                       int W, float* img, uint8_t* u8, int* range_flag) {
   __shared__ float ws[9 * 64 * 3];  // [tap][c][co]
   for (int i = threadIdx.x; i < 9 * 64 * 3; i += 256) {
     const int co = i % 3, c = (i / 3) % 64, tap = i / 192;
@@ -798,6 +818,7 @@ __global__ __launch_bounds__(256) void vae_tail_kernel(const float* in, const fl
       }
     }
   }
+  flag_nonfinite(range_flag, a0 + a1 + a2);
   const float o[3] = {1.f / (1.f + expf(-a0)), 1.f / (1.f + expf(-a1)), 1.f / (1.f + expf(-a2))};
   for (int co = 0; co < 3; ++co) {
     if (img != nullptr) img[((size_t)n * 3 + co) * H * W + pix] = o[co];
@@ -815,9 +836,10 @@ __global__ __launch_bounds__(256) void vae_tail_kernel(const float* in, const fl
 // 0.5 * sum_{c,y,x}(exp(lv) + mu^2 - 1 - lv) / (H_img * W_img).  One block per sample; the KL
 // sum is reduced in a fixed order (per-thread strided partials, then a fixed tree).
 // in: materialised GELU(GN(enc.15)) NHWC [N][HW][256].
-__global__ __launch_bounds__(256) void vae_enc_tail_kernel(const float* in, const float* wmu, const float* bmu,
+static __global__ __launch_bounds__(256) void vae_enc_tail_kernel(const float* in, const float* wmu, const float* bmu,
                                                            const float* wlv, const float* blv, const float* eps,
-                                                           float* z, float* kl, int HW, float scale, float inv_px) {
+                                                           float* z, float* kl, int HW, float scale, float inv_px,
+                                                           int* range_flag) {
   __shared__ float ws[8][256];  // rows 0-3: to_mu, 4-7: to_logvar ([out][in] of the 1x1 convs)
   __shared__ float red[256];
   for (int i = threadIdx.x; i < 8 * 256; i += 256) ws[i / 256][i % 256] = i < 1024 ? wmu[i] : wlv[i - 1024];
@@ -841,6 +863,7 @@ __global__ __launch_bounds__(256) void vae_enc_tail_kernel(const float* in, cons
     }
 #pragma unroll
     for (int o = 0; o < 4; ++o) {
+      flag_nonfinite(range_flag, a[o] + a[o + 4]);
       const float mu = a[o], lv = fminf(fmaxf(a[o + 4], -30.f), 20.f);
       const size_t idx = ((size_t)n * 4 + o) * HW + pix;
       z[idx] = (mu + eps[idx] * expf(0.5f * lv)) * scale;
@@ -860,7 +883,7 @@ __global__ __launch_bounds__(256) void vae_enc_tail_kernel(const float* in, cons
 //   kind 0: Conv2d [Cout][Cin][KS][KS], k = (ky*KS+kx)*Cin + c
 //   kind 1: Linear [Cout][Cin],        k = c
 //   kind 2: ConvTranspose2d(4,s2,p1) [Cin][Cout][4][4], phase (py,px), tap (jy,jx)
-__global__ void repack_kernel(float* dst, const float* src, int kind, int P, int Npad, int Kpad, int Cout, int Cin,
+static __global__ void repack_kernel(float* dst, const float* src, int kind, int P, int Npad, int Kpad, int Cout, int Cin,
                               int KS) {
   const size_t total = (size_t)P * Npad * Kpad;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
@@ -886,7 +909,7 @@ __global__ void repack_kernel(float* dst, const float* src, int kind, int P, int
 }
 
 // Transpose [R][Cc] -> [Cc][R] (embedding weights for coalesced access).
-__global__ void transpose_kernel(float* dst, const float* src, int R, int Cc) {
+static __global__ void transpose_kernel(float* dst, const float* src, int R, int Cc) {
   const size_t total = (size_t)R * Cc;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
     const int r = (int)(i / Cc), c = (int)(i % Cc);
@@ -894,7 +917,39 @@ __global__ void transpose_kernel(float* dst, const float* src, int R, int Cc) {
   }
 }
 
-__global__ void decrement_t_kernel(int64_t* t) {
+// Latent-channel frames of generate_steps.py:47-64 (save_latent_channels_by_dir): per (sample,
+// channel) min-max normalisation ch_norm = (ch - min) / (max - min) (0 where max == min), then
+// numpy's (ch_norm * 255).astype(uint8) (float32 product, truncation toward zero).  One rounding
+// per reference op (IEEE division), so the bytes equal the reference's.  One block per (n, c).
+static __global__ __launch_bounds__(256) void latent_frames_kernel(const float* z, uint8_t* out, int HW) {
+  __shared__ float smin[256], smax[256];
+  const float* ch = z + (size_t)blockIdx.x * HW;
+  float lo = 3.402823466e38f, hi = -3.402823466e38f;
+  for (int i = threadIdx.x; i < HW; i += 256) {
+    const float v = ch[i];
+    lo = fminf(lo, v);
+    hi = fmaxf(hi, v);
+  }
+  smin[threadIdx.x] = lo;
+  smax[threadIdx.x] = hi;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      smin[threadIdx.x] = fminf(smin[threadIdx.x], smin[threadIdx.x + s]);
+      smax[threadIdx.x] = fmaxf(smax[threadIdx.x], smax[threadIdx.x + s]);
+    }
+    __syncthreads();
+  }
+  lo = smin[0];
+  hi = smax[0];
+  const float den = rnd(hi - lo);
+  for (int i = threadIdx.x; i < HW; i += 256) {
+    const float nrm = hi > lo ? rnd(ch[i] - lo) / den : 0.f;
+    out[(size_t)blockIdx.x * HW + i] = (uint8_t)rnd(nrm * 255.f);
+  }
+}
+
+static __global__ void decrement_t_kernel(int64_t* t) {
   if (threadIdx.x == 0 && blockIdx.x == 0) *t = *t - 1;
 }
 

@@ -1,0 +1,32 @@
+// dmx — host launchers of the templated kernel families.  Each family is instantiated in its
+// own translation unit (k_*.hip) so the library builds in parallel; engine.hip only calls
+// these functions.
+#pragma once
+#include "common.h"
+#include "igemm.h"
+#include "igemm_x3.h"
+#include "tokmlp.h"
+
+namespace dmx {
+
+// split-precision implicit GEMM (igemm_x3.h): bm, bn in {64, 128}; sa = A from f16 hi/lo planes;
+// x1 = config-4 fp16 arithmetic.  k_x3_stats.hip (EPI_STATS), k_x3_part.hip (EPI_PARTIAL),
+// k_x3_epi.hip (EPI_BIAS / EPI_BIAS_GELU / EPI_BIAS_RES).
+void launch_x3_stats(int bm, int bn, int sa, int x1, const X3Params& p, dim3 grid, hipStream_t st);
+void launch_x3_partial(int bm, int bn, int sa, int x1, const X3Params& p, dim3 grid, hipStream_t st);
+void launch_x3_epi(int epi, int bm, int bn, int sa, int x1, const X3Params& p, dim3 grid, hipStream_t st);
+// 512-thread ping-pong split-precision GEMM (igemm_pp.h), EPI_STATS, 256 x bn tiles.
+void launch_pp(int bn, int sa, int x1, const X3Params& p, dim3 grid, hipStream_t st);
+// exact-fp32 MFMA implicit GEMM (igemm.h), k_f32.hip.
+void launch_f32(int src_mode, int epi, int bm, int bn, const IgemmParams& p, dim3 grid, hipStream_t st);
+// attention cores (k_attn.hip): split-precision (D, waves-per-EU hint, x1) and exact fp32 (D, QT).
+void launch_attention_x3(int D, int wpe, int x1, const float* qkv, float* out, int L, int C, dim3 grid,
+                         hipStream_t st);
+void launch_attention_f32(int D, int qt, const float* qkv, float* out, int L, int C, dim3 grid, hipStream_t st);
+// fused attention-block token kernels (tokmlp.h), k_tok.hip.
+void launch_tok_qkv_lds(int C, int tpb, int x1, const TokParams& tp, dim3 grid, hipStream_t st);
+void launch_tok_qkv(int C, int nb, int x1, const TokParams& tp, dim3 grid, hipStream_t st);
+void launch_tok_out(int C, int tm, int x1, int nw, int lds, int tpb, const TokParams& tp, int blocks,
+                    hipStream_t st);
+
+}  // namespace dmx

@@ -46,19 +46,27 @@ def broadcast_module(module: torch.nn.Module, src: int = 0) -> None:
 
 def gather_rows(local: torch.Tensor, total: int, dst: int = 0) -> Optional[torch.Tensor]:
     """C2: concatenate every rank's shard (dim 0) on `dst` in global order; None elsewhere.
-    Shards may differ by one row; they are padded to a common size for the collective."""
+
+    One ``dist.gather`` to `dst` (only `dst` receives the shards).  Shards may differ by one
+    row, and ranks beyond `total` hold an empty shard: every shard is padded to the largest
+    size so the collective is uniform, and `dst` trims the padding.  With the gloo backend the
+    shards travel through host memory (gloo's gather is CPU-only)."""
     ws, rank = world()
     if ws == 1:
         return local
     sizes = [shard_range(total, ws, r)[1] - shard_range(total, ws, r)[0] for r in range(ws)]
-    mx = max(sizes)
-    pad = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    if local.shape[0] != sizes[rank]:
+        raise ValueError(f"rank {rank}: shard has {local.shape[0]} rows, shard_range gives {sizes[rank]}")
+    dev = local.device
+    if dist.get_backend() == "gloo" and local.is_cuda:
+        local = local.cpu()
+    pad = torch.zeros((max(sizes),) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
     pad[: local.shape[0]] = local
-    bufs = [torch.empty_like(pad) for _ in range(ws)]
-    dist.all_gather(bufs, pad)
+    bufs = [torch.empty_like(pad) for _ in range(ws)] if rank == dst else None
+    dist.gather(pad, gather_list=bufs, dst=dst)
     if rank != dst:
         return None
-    return torch.cat([b[:s] for b, s in zip(bufs, sizes)], dim=0)
+    return torch.cat([b[:s] for b, s in zip(bufs, sizes)], dim=0).to(dev)
 
 
 def host_noise_slice(shape_global, start: int, end: int, device) -> torch.Tensor:
@@ -88,8 +96,13 @@ class ShardedCondSampler:
     def __init__(self, diffuser, model, vae=None):
         self.d, self.model, self.vae = diffuser, model, vae
 
-    def sample(self, class_counts, z_shape, guidance_scale: float = 3.0, null_label: int = 0, cond=None,
-               cond_mask=None, decode: bool = True) -> Optional[torch.Tensor]:
+    def sample(self, class_counts, z_shape=None, guidance_scale: float = 3.0, null_label: int = 0, cond=None,
+               cond_mask=None, decode: bool = True, dummy_input_hw=(224, 224)) -> Optional[torch.Tensor]:
+        """Arguments as Diffuser.sample_latent_cond (diff.py:174-369); returns on rank 0 the
+        (B, 8H, 8W, 3) uint8 images (decode and a VAE given) or the (B, C, H, W) latents,
+        None on the other ranks.  Draw order per rank equals the single-process sampler's
+        (optional encode draw, x_T, then the seed (device mode) or one global draw per step
+        (host mode)), so rank 0's result is the single-process result."""
         ws, rank = world()
         d = self.d
         items = d._norm_counts(class_counts)
@@ -101,26 +114,39 @@ class ShardedCondSampler:
         vals, msk = d._build_cond(y_list, cond, cond_mask, None, None, dev)
         s, e = shard_range(B, ws, rank)
         y = torch.tensor(y_list[s:e], device=dev, dtype=torch.long)
-        v, m = vals[s:e].contiguous().float(), msk[s:e].contiguous().float()
+        v, m = vals[s:e].float().contiguous(), msk[s:e].float().contiguous()
+        if z_shape is None:
+            if self.vae is None:
+                raise ValueError("z_shape 省略時は vae が必要です。")
+            z_shape = d._latent_shape(self.vae, dummy_input_hw, dev)
         C, H, W = z_shape
-        nm = self.model.native()
+        nm = self.model.native() if e > s else None
         tables = d.coef_tables(dev, clamp_prev=True)
+        x = torch.randn((B, C, H, W))[s:e].to(dev).contiguous()  # x_T (diff.py:327), global draw
         if d.noise_source == "device":
-            seed = torch.tensor([d._seed()], dtype=torch.long, device=dev)
+            seed = torch.tensor([d._seed()], dtype=torch.long)  # drawn after x_T, as _run_cond_loop does
             if ws > 1:
+                if dist.get_backend() != "gloo":
+                    seed = seed.to(dev)
                 dist.broadcast(seed, src=0)
-            x = torch.randn((B, C, H, W))[s:e].to(dev).contiguous()
-            t_dev = torch.full((1,), d.num_timesteps, dtype=torch.long, device=dev)
-            nm.sample_loop(x, t_dev, y, null_label, v, m, float(guidance_scale), tables, d.num_timesteps,
-                           seed=int(seed.item()), sample_offset=s, use_graph=d.use_graph)
+            if e > s:
+                t_dev = torch.full((1,), d.num_timesteps, dtype=torch.long, device=dev)
+                nm.sample_loop(x, t_dev, y, null_label, v, m, float(guidance_scale), tables, d.num_timesteps,
+                               seed=int(seed.item()), sample_offset=s, use_graph=d.use_graph)
         else:
             def step(xs, t, noise):
+                if xs.shape[0] == 0:  # empty shard (B < world size): nothing to compute
+                    return xs
                 out = torch.empty_like(xs)
                 tt = torch.full((xs.shape[0],), t, dtype=torch.long, device=dev)
                 nm.step(xs, out, tt, y, null_label, v, m, float(guidance_scale), tables, noise)
                 return out
-            x = sharded_loop(step, (B, C, H, W), d.num_timesteps, dev, "host")
+            for i in range(d.num_timesteps, 0, -1):
+                x = step(x, i, host_noise_slice((B, C, H, W), s, e, dev))
         if decode and self.vae is not None:
-            _, u8 = self.vae.native().decode(x, want_img=False, want_u8=True)
+            if e > s:
+                _, u8 = self.vae.native().decode(x, want_img=False, want_u8=True)
+            else:
+                u8 = torch.empty((0, 8 * H, 8 * W, 3), dtype=torch.uint8, device=dev)
             return gather_rows(u8, B)
         return gather_rows(x, B)

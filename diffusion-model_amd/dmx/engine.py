@@ -5,6 +5,7 @@ moves pointers: torch provides device memory and streams.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import threading
@@ -76,7 +77,8 @@ def require_cuda(t: torch.Tensor, what: str) -> None:
 class NativeModel:
     """A repacked copy of one reference network inside libdmx (U-Net or VAE)."""
 
-    def __init__(self, kind: int, params: Dict[str, torch.Tensor], in_ch: int = 4, remove_deep_conv: bool = False):
+    def __init__(self, kind: int, params: Dict[str, torch.Tensor], in_ch: int = 4, remove_deep_conv: bool = False,
+                 **cfg):
         self.kind = kind
         self.in_ch = in_ch
         some = next(iter(params.values()))
@@ -85,7 +87,9 @@ class NativeModel:
         self.ctx = Context.get(self.device)
         self.lib = self.ctx.lib
         h = ctypes.c_void_p()
-        check(self.lib.dmx_model_create(self.ctx.handle, kind, in_ch, int(remove_deep_conv), ctypes.byref(h)))
+        conf = _lib.ModelConfig.make(kind, in_ch, remove_deep_conv, **cfg)
+        self.geom_dim = int(conf.geom_dim)
+        check(self.lib.dmx_model_create_cfg(self.ctx.handle, ctypes.byref(conf), ctypes.byref(h)))
         self.handle = h
         keep = []
         for name, t in params.items():
@@ -110,6 +114,24 @@ class NativeModel:
         operands rounded to fp16, one MFMA, fp32 accumulate; norms, softmax and the scheduler stay fp32)."""
         code = self.PRECISIONS[prec] if isinstance(prec, str) else int(prec)
         check(self.lib.dmx_model_set_precision(self.handle, code))
+
+    def range_tripped(self, reset: bool = True) -> bool:
+        """True when an output kernel saw a non-finite value since the last reset (include/dmx.h
+        dmx_model_range_check: the split-precision range guard).  Synchronises the current stream."""
+        f = ctypes.c_int(0)
+        with torch.cuda.device(self.device):
+            check(self.lib.dmx_model_range_check(self.handle, int(reset), ctypes.byref(f),
+                                                 ctypes.c_void_p(_stream(self.device))))
+        return bool(f.value)
+
+    @contextlib.contextmanager
+    def precision_override(self, prec):
+        old = self.precision
+        self.set_precision(prec)
+        try:
+            yield self
+        finally:
+            self.set_precision(old)
 
     @property
     def precision(self) -> str:
@@ -139,7 +161,7 @@ class NativeModel:
             vals = vals.to(device=x.device, dtype=torch.float32).contiguous()
             mask = mask.to(device=x.device, dtype=torch.float32).contiguous()
         eps = torch.empty_like(x)
-        geom = torch.empty((n, 12), device=x.device, dtype=torch.float32) if want_geom else None
+        geom = torch.empty((n, self.geom_dim), device=x.device, dtype=torch.float32) if want_geom else None
         with torch.cuda.device(x.device):
             check(self.lib.dmx_unet_forward(self.handle, _ptr(x), _ptr(t), _ptr(y), _ptr(vals), _ptr(mask),
                                             _ptr(eps), _ptr(geom), n, h, w, ctypes.c_void_p(_stream(x.device))))
@@ -165,6 +187,24 @@ class NativeModel:
         finally:
             check(self.lib.dmx_debug_enable(self.handle, 0))
 
+    def _norm_inputs(self, x_in, t, y, vals, mask, noise):
+        """The kernels read raw bytes: t / y as contiguous int64, vals / mask / noise as contiguous fp32,
+        all on x's device (a bool cond_mask, float64 values or a column slice are converted here, as the
+        reference's torch.cat / arithmetic would promote them).  The converted tensors are kept alive on
+        the model until the next call so the enqueued launches never read freed memory."""
+        dev = x_in.device
+        t = t.to(device=dev, dtype=torch.long).contiguous()
+        if y is not None:
+            y = y.to(device=dev, dtype=torch.long).contiguous()
+        if vals is not None:
+            vals = vals.to(device=dev, dtype=torch.float32).contiguous()
+        if mask is not None:
+            mask = mask.to(device=dev, dtype=torch.float32).contiguous()
+        if noise is not None:
+            noise = noise.to(device=dev, dtype=torch.float32).contiguous()
+        self._live = (t, y, vals, mask, noise)
+        return t, y, vals, mask, noise
+
     def _args(self, x_in, x_out, t, t_stride, y, null_label, vals, mask, guidance, tables, noise, seed,
               sample_offset) -> StepArgs:
         c1, c2, sd = tables
@@ -187,6 +227,9 @@ class NativeModel:
              sample_offset=0, t_stride=1):
         """One denoising step: CFG (2n batched forward) when guidance > 0 and y given."""
         self.ctx.ensure_time_table(int(tables[0].numel()))
+        _check_state(x_in, "x")
+        _check_state(x_out, "x_out")
+        t, y, vals, mask, noise = self._norm_inputs(x_in, t, y, vals, mask, noise)
         a = self._args(x_in, x_out, t, t_stride, y, null_label, vals, mask, guidance, tables, noise, seed,
                        sample_offset)
         with torch.cuda.device(x_in.device):
@@ -196,6 +239,7 @@ class NativeModel:
                      t_stride=1, cap=1024):
         """One eager step with event timing per launch -> list of dicts."""
         self.ctx.ensure_time_table(int(tables[0].numel()))
+        t, y, vals, mask, noise = self._norm_inputs(x_in, t, y, vals, mask, noise)
         a = self._args(x_in, x_out, t, t_stride, y, null_label, vals, mask, guidance, tables, noise, seed, 0)
         recs = (_lib.KernelRecord * cap)()
         n = ctypes.c_int()
@@ -216,10 +260,18 @@ class NativeModel:
         decremented on the device after each step.  Runs on a side stream (graph capture
         needs a non-default stream) ordered against the current stream."""
         self.ctx.ensure_time_table(int(tables[0].numel()))
+        _check_state(x, "x")
+        if t_dev.dtype != torch.long or not t_dev.is_contiguous() or t_dev.device != x.device:
+            raise ValueError("sample_loop: t_dev must be a contiguous int64 device scalar on x's device "
+                             "(it is decremented in place)")
+        _, y, vals, mask, _ = self._norm_inputs(x, t_dev, y, vals, mask, None)
         a = self._args(x, x, t_dev, 0, y, null_label, vals, mask, guidance, tables, None, seed, sample_offset)
         cur = torch.cuda.current_stream(x.device)
         side = self.side_stream()
         side.wait_stream(cur)
+        for keep in (x, t_dev, y, vals, mask) + tuple(tables):
+            if keep is not None:
+                keep.record_stream(side)
         with torch.cuda.device(x.device):
             check(self.lib.dmx_sample_loop(self.handle, ctypes.byref(a), int(steps), int(use_graph),
                                            ctypes.c_void_p(side.cuda_stream)))
@@ -236,6 +288,17 @@ class NativeModel:
                                           ctypes.c_void_p(_stream(z.device))))
         return img, u8
 
+    def decode_u8_into(self, z, u8) -> None:
+        """Decode z (n,4,h,w) straight into a caller-owned uint8 (n,8h,8w,3) HWC buffer."""
+        n, c, h, w = z.shape
+        zc = z.contiguous().float()
+        if u8.dtype != torch.uint8 or not u8.is_contiguous() or tuple(u8.shape) != (n, 8 * h, 8 * w, 3):
+            raise ValueError(f"u8 must be a contiguous uint8 tensor of shape {(n, 8 * h, 8 * w, 3)}")
+        with torch.cuda.device(zc.device):
+            check(self.lib.dmx_vae_decode(self.handle, _ptr(zc), None, _ptr(u8), n, h, w,
+                                          ctypes.c_void_p(_stream(zc.device))))
+        self._live_dec = zc
+
     def encode(self, x, eps) -> Tuple[torch.Tensor, torch.Tensor]:
         """x (n,3,h,w), eps (n,4,h/8,w/8) -> (z, per-sample KL (n,)) (models/vae.py:51-62)."""
         n, c, h, w = x.shape
@@ -249,17 +312,37 @@ class NativeModel:
         return z, kl
 
 
+def _check_state(x: torch.Tensor, what: str) -> None:
+    """The step kernels read / write x as contiguous fp32 NCHW on the device."""
+    require_cuda(x, what)
+    if x.dtype != torch.float32 or not x.is_contiguous():
+        raise ValueError(f"{what} must be a contiguous float32 tensor (got {x.dtype}, contiguous={x.is_contiguous()})")
+
+
 def ddpm_update(x, eu, ec, guidance, t, tables, noise=None, seed=0, sample_offset=0):
-    """Standalone K1 (diff.py:151,158-162) for duck-typed models: returns x'."""
+    """Standalone K1 (diff.py:151,158-162) for duck-typed models: returns x'.
+
+    Every converted operand is bound to a local for the duration of the launch (a temporary
+    freed right after taking its pointer could be handed to the next conversion by the
+    caching allocator)."""
     lib = _lib.load()
     c1, c2, sd = tables
-    n, c, h, w = x.shape
-    out = torch.empty_like(x)
-    t = t.to(device=x.device, dtype=torch.long).contiguous()
-    with torch.cuda.device(x.device):
-        check(lib.dmx_ddpm_update(_ptr(x.contiguous()), _ptr(out), _ptr(eu.contiguous().float()),
-                                  _ptr(ec.contiguous().float() if ec is not None else None), float(guidance), _ptr(t),
-                                  1, _ptr(c1), _ptr(c2), _ptr(sd), int(c1.numel()),
-                                  _ptr(noise.contiguous() if noise is not None else None), int(seed),
-                                  int(sample_offset), n, c, h, w, ctypes.c_void_p(_stream(x.device))))
+    require_cuda(x, "x")
+    dev = x.device
+    x_c = x.to(dtype=torch.float32).contiguous()
+    n, c, h, w = x_c.shape
+    eu_c = eu.to(device=dev, dtype=torch.float32).contiguous()
+    ec_c = ec.to(device=dev, dtype=torch.float32).contiguous() if ec is not None else None
+    nz_c = noise.to(device=dev, dtype=torch.float32).contiguous() if noise is not None else None
+    t_c = t.to(device=dev, dtype=torch.long).contiguous()
+    for e, nm in ((eu_c, "eps"), (ec_c, "eps_cond"), (nz_c, "noise")):
+        if e is not None and tuple(e.shape) != tuple(x_c.shape):
+            raise ValueError(f"{nm} shape {tuple(e.shape)} != x shape {tuple(x_c.shape)}")
+    if t_c.numel() != n:
+        raise ValueError(f"t has {t_c.numel()} entries for a batch of {n}")
+    out = torch.empty_like(x_c)
+    with torch.cuda.device(dev):
+        check(lib.dmx_ddpm_update(_ptr(x_c), _ptr(out), _ptr(eu_c), _ptr(ec_c), float(guidance), _ptr(t_c),
+                                  1, _ptr(c1), _ptr(c2), _ptr(sd), int(c1.numel()), _ptr(nz_c), int(seed),
+                                  int(sample_offset), n, c, h, w, ctypes.c_void_p(_stream(dev))))
     return out

@@ -1,16 +1,18 @@
 """Drop-in ``models.unet_cond`` (reference models/unet_cond.py:102-216).
 
-``UnetCond`` keeps the reference constructor, attributes and state_dict keys;
-its forward runs the native U-Net of libdmx (conv3x3+GroupNorm+GELU residual
-blocks, 4-head self-attention at six resolutions, sinusoidal time + class +
+``UnetCond`` keeps the reference constructor, attributes, module tree, default
+initialisation (drawn from the global torch generator in the reference's order) and
+state_dict keys; its forward runs the native U-Net of libdmx (conv3x3+GroupNorm+GELU
+residual blocks, 4-head self-attention at six resolutions, sinusoidal time + class +
 geometric-condition embedding) and returns eps like the reference.
 """
 from __future__ import annotations
 
 import torch
 
-from dmx import _lib, spec
-from models._native import NativeBacked, build_param_tree
+from dmx import _lib
+from models._modules import AttenionBlock, Down, ResBlock, Up, build_cond_embedding, build_unet_body  # noqa: F401
+from models._native import NativeBacked
 
 
 class UnetCond(NativeBacked):
@@ -20,17 +22,25 @@ class UnetCond(NativeBacked):
 
     def __init__(self, in_ch=4, time_dim=256, num_classes=3, cfg_drop_prob=0.1, remove_deep_conv=False):
         super().__init__()
-        if time_dim != 256 or num_classes != 3:
-            raise ValueError("dmx implements the reference configuration time_dim=256, num_classes=3")
         self.time_dim = time_dim
         self.remove_deep_conv = remove_deep_conv
         self.num_classes = num_classes
         self.cfg_drop_prob = cfg_drop_prob
         self._dmx_in_ch = in_ch
-        build_param_tree(self, self._spec(in_ch, remove_deep_conv))
+        build_cond_embedding(self, num_classes, time_dim)
+        build_unet_body(self, in_ch, remove_deep_conv)
 
-    def _spec(self, in_ch, remove_deep_conv):
-        return spec.unet_cond_spec(in_ch=in_ch, remove_deep_conv=remove_deep_conv)
+    def _dmx_config(self) -> dict:
+        return {"num_classes": self.num_classes}
+
+    def _dmx_check_supported(self) -> None:
+        if self.time_dim != 256:
+            # the reference's Down/Up emb heads are Linear(256, .) whatever time_dim is
+            # (models/unet_cond.py:55,73), so its forward fails for any other width as well
+            raise RuntimeError(f"time_dim={self.time_dim}: the reference's emb_layer heads take 256 inputs "
+                               f"(models/unet_cond.py:64,84); only time_dim=256 has a forward pass")
+        if not 1 <= self._dmx_in_ch <= 4:
+            raise NotImplementedError(f"dmx implements in_ch in [1, 4] (got {self._dmx_in_ch})")
 
     def _check_training(self, cond_drop_prob=None):
         p = self.cfg_drop_prob if cond_drop_prob is None else cond_drop_prob

@@ -3,7 +3,8 @@ from __future__ import annotations
 
 import torch
 
-from dmx import _lib, spec
+from dmx import _lib
+from models._modules import GeomHead
 from models.unet_cond import UnetCond
 
 
@@ -14,14 +15,13 @@ class UnetCondWithGeomHead(UnetCond):
 
     def __init__(self, in_ch=4, time_dim=256, num_classes=3, cfg_drop_prob=0.0, remove_deep_conv=False,
                  geom_dim=12, geom_hidden=256):
-        if geom_dim != 12 or geom_hidden != 256:
-            raise ValueError("dmx implements the reference GeomHead geom_dim=12, geom_hidden=256")
-        self._geom_dim, self._geom_hidden = geom_dim, geom_hidden
         super().__init__(in_ch=in_ch, time_dim=time_dim, num_classes=num_classes, cfg_drop_prob=cfg_drop_prob,
                          remove_deep_conv=remove_deep_conv)
+        self.geom_head = GeomHead(in_ch=64, out_dim=geom_dim, hidden=geom_hidden)
+        self._geom_dim, self._geom_hidden = geom_dim, geom_hidden
 
-    def _spec(self, in_ch, remove_deep_conv):
-        return spec.unet_cond_geom_spec(in_ch=in_ch, remove_deep_conv=remove_deep_conv)
+    def _dmx_config(self) -> dict:
+        return {"num_classes": self.num_classes, "geom_dim": self._geom_dim, "geom_hidden": self._geom_hidden}
 
     def forward(self, x: torch.Tensor, t: torch.Tensor, y: torch.Tensor, cond_vals: torch.Tensor = None,
                 cond_mask: torch.Tensor = None, cond_drop_prob: float = 0.0):

@@ -14,8 +14,9 @@ from __future__ import annotations
 
 import torch
 
-from dmx import _lib, spec
-from models._native import NativeBacked, build_param_tree
+from dmx import _lib
+from models._modules import build_vae
+from models._native import NativeBacked
 
 
 def latent_hw(h: int, w: int):
@@ -31,11 +32,18 @@ class VAE(NativeBacked):
 
     def __init__(self, in_channels=3, z_channels=4, base_channels=64, scale_factor=0.18215):
         super().__init__()
-        if (in_channels, z_channels, base_channels) != (3, 4, 64) or scale_factor != 0.18215:
-            raise ValueError("dmx implements the reference VAE configuration (3, 4, 64, 0.18215)")
         self.z_channels = z_channels
         self.scale_factor = scale_factor
-        build_param_tree(self, spec.vae_spec(in_channels, z_channels, base_channels), seed=1)
+        self._dmx_shape = (in_channels, z_channels, base_channels)
+        build_vae(self, in_channels, z_channels, base_channels)
+
+    def _dmx_config(self) -> dict:
+        return {"scale_factor": float(self.scale_factor)}
+
+    def _dmx_check_supported(self) -> None:
+        if self._dmx_shape != (3, 4, 64):
+            raise NotImplementedError("dmx implements the reference VAE widths in_channels=3, z_channels=4, "
+                                      f"base_channels=64 (got {self._dmx_shape}); scale_factor is free")
 
     # ---- native ------------------------------------------------------------------------
     def decode(self, z: torch.Tensor) -> torch.Tensor:

@@ -64,6 +64,25 @@ int dmx_model_key(int kind, int in_ch, int remove_deep_conv, int index, char* na
                   int64_t* shape_out /* [4] */, int* ndim_out);
 
 int dmx_model_create(dmx_ctx* ctx, int kind, int in_ch, int remove_deep_conv, dmx_model** out);
+
+/* Constructor arguments of the reference networks that change the checkpoint layout or
+ * the arithmetic (UnetCond / UnetCondWithGeomHead / VAE __init__, reference
+ * models/unet_cond.py:113, models/unet_cond_geom.py:31-49, models/vae.py:11).
+ * dmx_model_create(..) is dmx_model_create_cfg with the reference defaults
+ * (num_classes 3, geom_dim 12, geom_hidden 256, scale_factor 0.18215). */
+typedef struct dmx_model_config {
+  int kind;             /* DMX_UNET_COND_GEOM .. DMX_VAE */
+  int in_ch;            /* U-Net latent channels, 1..4 */
+  int remove_deep_conv; /* models/unet_cond.py:139-145 */
+  int num_classes;      /* class_emb has num_classes + 1 rows (models/unet_cond.py:121) */
+  int geom_dim;         /* GeomHead output width (models/unet_cond_geom.py:38) */
+  int geom_hidden;      /* GeomHead hidden width (models/unet_cond_geom.py:39) */
+  float scale_factor;   /* VAE latent scale (models/vae.py:11,59,66) */
+} dmx_model_config;
+int dmx_model_create_cfg(dmx_ctx* ctx, const dmx_model_config* cfg, dmx_model** out);
+int dmx_model_cfg_num_keys(const dmx_model_config* cfg);
+int dmx_model_cfg_key(const dmx_model_config* cfg, int index, char* name_out, int name_cap,
+                      int64_t* shape_out /* [4] */, int* ndim_out);
 int dmx_model_destroy(dmx_model* m);
 /* Register one reference-layout tensor (device pointer, fp32 contiguous). */
 int dmx_model_set_tensor(dmx_model* m, const char* name, const float* dev_ptr, const int64_t* shape, int ndim);
@@ -74,6 +93,11 @@ int dmx_model_finalize(dmx_model* m, void* stream);
  * 2 = fp16 operands (BASELINE config 4: one MFMA, fp32 accumulate, fp32 norms/softmax/scheduler). */
 int dmx_model_set_precision(dmx_model* m, int prec);
 int dmx_model_get_precision(const dmx_model* m);
+/* Range guard of the split-precision modes (1, 2): an operand beyond the f16 range turns a
+ * network output (eps / decoded pixel / encoder head) non-finite, and the output kernels then
+ * raise a sticky per-model flag.  Reads it (synchronising `stream`), optionally clearing it;
+ * the Python samplers check it at chunk boundaries and recompute the chunk in mode 0. */
+int dmx_model_range_check(dmx_model* m, int reset, int* flagged, void* stream);
 
 /* ---- U-Net forward (replaces model(x, t, y, cond_vals, cond_mask), diff.py:149-150) --
  * x: (n,in_ch,h,w); t: (n,) int64 in [1, tmax]; y: (n,) int64 or NULL (DMX_UNET);
@@ -122,6 +146,11 @@ int dmx_ddpm_update(const float* x, float* x_out, const float* eu, const float* 
  * x*255 -> clamp -> uint8, diff.py:58-62) ---------------------------------------------
  * z: (n,4,h,w); img: (n,3,8h,8w) fp32 or NULL; u8: (n,8h,8w,3) uint8 (HWC) or NULL. */
 int dmx_vae_decode(dmx_model* m, const float* z, float* img, uint8_t* u8, int n, int h, int w, void* stream);
+
+/* ---- latent-channel frames (replaces generate_steps.py:47-64 save_latent_channels_by_dir's
+ * per-channel min-max -> *255 -> uint8 before the PNG write) ---------------------------------
+ * z: (n,c,h,w) fp32 device; out: (n,c,h,w) uint8 device, byte-identical to the reference's. */
+int dmx_latent_frames_u8(const float* z, uint8_t* out, int n, int c, int h, int w, void* stream);
 
 /* ---- VAE encode (replaces VAE.encode, vae.py:51-62) -------------
  * x: (n,3,h,w) fp32, h and w multiples of 8; eps: (n,4,h/8,w/8) = the reference's

@@ -90,3 +90,74 @@ def test_host_noise_is_shard_invariant_world2():
     for i in range(6, 0, -1):
         x = _toy_step(x, i, torch.randn((5, 2, 3, 3)))
     assert torch.equal(res[0], x)
+
+
+# ---- ShardedCondSampler plumbing with a stub native model (CPU) -------------------------
+class _FakeNative:
+    """Stands in for dmx NativeModel: a per-sample deterministic step (the real one is covered by
+    tests/test_gpu_multi.py on the GPU)."""
+
+    def step(self, xs, out, tt, y, null_label, v, m, g, tables, noise):
+        out.copy_(0.9 * xs + 0.1 * noise + 0.01 * y.view(-1, 1, 1, 1) + 0.001 * (v * m).sum(1).view(-1, 1, 1, 1))
+
+    def sample_loop(self, x, t_dev, y, null_label, v, m, g, tables, steps, seed=0, sample_offset=0, use_graph=True):
+        idx = torch.arange(sample_offset, sample_offset + x.shape[0], dtype=torch.float32).view(-1, 1, 1, 1)
+        x.mul_(0.5).add_(idx + float(seed % 997) * 1e-3 + 0.01 * y.view(-1, 1, 1, 1))
+        t_dev.sub_(steps)
+
+    def decode(self, x, want_img=False, want_u8=True):
+        u8 = (x.mean(1, keepdim=True).clamp(0, 1) * 255).to(torch.uint8).expand(-1, 3, -1, -1)
+        u8 = u8.repeat_interleave(8, 2).repeat_interleave(8, 3).permute(0, 2, 3, 1).contiguous()
+        return None, u8
+
+
+class _FakeModel:
+    _n = _FakeNative()
+
+    def native(self):
+        return self._n
+
+
+def _sharded_sampler(rank, world, B=5, mode="host", decode=True):
+    import diff
+    d = diff.Diffuser(4, device="cpu")
+    d.noise_source = mode
+    torch.manual_seed(7)
+    s = dd.ShardedCondSampler(d, _FakeModel(), _FakeModel() if decode else None)
+    counts = {1: B // 2 + B % 2, 3: B // 2} if B > 1 else (2, 1)
+    out = s.sample(counts, z_shape=(2, 3, 3), decode=decode)
+    return None if out is None else out.clone()
+
+
+def _sharded_b1(rank, world):
+    return _sharded_sampler(rank, world, B=1, mode="host", decode=True)
+
+
+def _sharded_device(rank, world):
+    return _sharded_sampler(rank, world, B=5, mode="device", decode=False)
+
+
+def _sharded_host_lat(rank, world):
+    return _sharded_sampler(rank, world, B=5, mode="host", decode=False)
+
+
+@pytest.mark.parametrize("fn", [_sharded_host_lat, _sharded_device, _sharded_b1])
+def test_sharded_sampler_world2_equals_single_process(fn):
+    """Rank 0 gets exactly the single-process result (host and device noise, decode, B < world)."""
+    res = run(fn)
+    single = fn(0, 1)
+    assert res[1] is None
+    assert torch.equal(res[0], single)
+
+
+def test_gather_rows_rejects_wrong_shard():
+    res = run(_bad_gather)
+    assert res[0] == "ValueError" and res[1] == "ValueError"
+
+
+def _bad_gather(rank, world):
+    try:
+        dd.gather_rows(torch.zeros(4, 2), 5)
+    except ValueError:
+        return "ValueError"
+    return "ok"

@@ -1,0 +1,111 @@
+"""The multi-GPU product path executed: ShardedCondSampler with world size 2 (gloo), both ranks on
+cuda:0 (a one-GPU rehearsal of the one-process-per-GPU layout; RCCL refuses two ranks on one
+device).  Rank 0 must receive the single-process result: latents within rel-L2 1e-5 (the shards
+run different batch sizes, so GEMM split-K choices — summation orders — may differ), decoded
+uint8 images within +-1 LSB.  Draw order per rank: tests/test_distributed_gloo.py (stub model)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _job(mode, decode, B=5, T=4):
+    import diff
+    from dmx import distributed as dd
+    from dmx import synth
+    from models.unet_cond_geom import UnetCondWithGeomHead
+    from models.vae import VAE
+    dev = torch.device("cuda:0")
+    m = UnetCondWithGeomHead()
+    m.load_state_dict(synth.unet_cond_geom_weights(0))
+    m.to(dev).eval()
+    v = None
+    if decode:
+        v = VAE()
+        v.load_state_dict(synth.vae_weights(1))
+        v.to(dev).eval()
+    d = diff.Diffuser(T, device=dev)
+    d.noise_source = mode
+    g = torch.Generator().manual_seed(40)
+    vals = torch.rand((B, 12), generator=g).to(dev)
+    mask = (torch.rand((B, 12), generator=g) > 0.3).float().to(dev)
+    torch.manual_seed(41)
+    out = dd.ShardedCondSampler(d, m, v).sample({1: 3, 3: B - 3}, z_shape=(4, 16, 16), cond=vals, cond_mask=mask,
+                                                decode=decode)
+    return None if out is None else out.cpu()
+
+
+def _worker(rank, world, port, mode, decode, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, _job(mode, decode)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run2(mode, decode):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, mode, decode, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("mode", ["host", "device"])
+def test_sharded_sampler_world2_on_one_gpu(cuda, mode):
+    res = _run2(mode, decode=True)
+    single = _job(mode, decode=True)
+    assert res[1] is None and res[0].shape == single.shape == (5, 128, 128, 3)
+    d = np.abs(res[0].numpy().astype(np.int32) - single.numpy().astype(np.int32))
+    assert d.max() <= 1 and (d > 0).mean() <= 1e-3, (int(d.max()), float((d > 0).mean()))
+
+
+def test_sharded_sampler_latents_world2_host(cuda):
+    res = _run2("host", decode=False)
+    single = _job("host", decode=False)
+    assert res[1] is None
+    assert float((res[0] - single).norm() / single.norm()) < 1e-5
+
+
+def test_sharded_world1_equals_diffuser_device_mode(cuda):
+    """same seed -> same samples from ShardedCondSampler (world 1) and
+    Diffuser.sample_latent_cond in device-noise mode (x_T drawn before the Philox seed in both)."""
+    import diff
+    from dmx import synth
+    from models.unet_cond_geom import UnetCondWithGeomHead
+    dev = torch.device("cuda:0")
+    lat = _job("device", decode=False)
+    m = UnetCondWithGeomHead()
+    m.load_state_dict(synth.unet_cond_geom_weights(0))
+    m.to(dev).eval()
+    d = diff.Diffuser(4, device=dev)
+    d.noise_source = "device"
+    g = torch.Generator().manual_seed(40)
+    vals = torch.rand((5, 12), generator=g).to(dev)
+    mask = (torch.rand((5, 12), generator=g) > 0.3).float().to(dev)
+    torch.manual_seed(41)
+    ref_lat = d.sample_latent_cond(m, {1: 3, 3: 2}, z_shape=(4, 16, 16), vae=None, progress=False, cond=vals,
+                                   cond_mask=mask)
+    assert torch.equal(lat, ref_lat.cpu())
