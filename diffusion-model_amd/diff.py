@@ -79,9 +79,36 @@ class Diffuser:
         return self._tables[key]
 
     # ---- RNG -------------------------------------------------------------------------------
+    _NOISE_RING = 3
+
     def _randn(self, shape, device):
-        """One Gaussian draw in the reference's order (host mode) — diff.py:104,158,327."""
-        return torch.randn(tuple(shape)).to(device)
+        """One Gaussian draw in the reference's order (host mode) — diff.py:104,158,327.
+
+        The draw is the global CPU generator's (torch.randn(shape, out=...) consumes it exactly like
+        torch.randn(shape)).  For a GPU destination it lands in a small ring of pinned host buffers
+        and goes up with a non-blocking copy, so the host draws step k+1's noise while the GPU runs
+        step k (a pageable copy would block the host until the stream drained)."""
+        shape = tuple(int(v) for v in shape)
+        dev = torch.device(device)
+        if dev.type != "cuda":
+            return torch.randn(shape).to(dev)
+        ring = self.__dict__.setdefault("_noise_ring", {})
+        key = (shape, str(dev))
+        slots = ring.get(key)
+        if slots is None:
+            slots = ring[key] = [[torch.empty(shape, pin_memory=True), None] for _ in range(self._NOISE_RING)]
+            self.__dict__.setdefault("_noise_next", {})[key] = 0
+        k = self._noise_next[key]
+        self._noise_next[key] = (k + 1) % len(slots)
+        buf, ev = slots[k]
+        if ev is not None:
+            ev.synchronize()  # the copy that last read this pinned slot has finished
+        torch.randn(shape, out=buf)
+        out = buf.to(dev, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        slots[k][1] = ev
+        return out
 
     def _step_noise(self, x):
         if self.noise_source == "host":

@@ -95,6 +95,7 @@ SIGNATURES = [
                              _I, _I, _I, _I, _P]),
     ("dmx_vae_decode", _I, [_P, _P, _P, _P, _I, _I, _I, _P]),
     ("dmx_latent_frames_u8", _I, [_P, _P, _I, _I, _I, _I, _P]),
+    ("dmx_eval_metrics", _I, [_P, _P, _I, _I, _I, _I, _I, _I, ctypes.c_double, _P, _P, _P]),
     ("dmx_vae_encode", _I, [_P, _P, _P, _P, _P, _I, _I, _I, _P]),
     ("dmx_model_workspace_bytes", _I64, [_P]),
     ("dmx_debug_enable", _I, [_P, _I]),

@@ -19,6 +19,7 @@
 #include "igemm_pp.h"
 #include "launch.h"
 #include "tokmlp.h"
+#include "eval.h"
 
 namespace dmx {
 
@@ -264,6 +265,9 @@ struct dmx_model {
   bool debug = false;
   int prec = 1;  // 0: fp32 MFMA (exact fp32 products), 1: fp16 hi/lo x3 split MFMA, 2: fp16 (config 4)
   int* range_flag = nullptr;  // device int: an output went non-finite (kernels.h flag_nonfinite)
+  // reduce_norm_mb_kernel hand-off state (partials + counters per source sample), grown on demand
+  dmx::RnSync rn{};
+  int rn_cap = 0, rn_need = 0;
   std::vector<std::pair<std::string, std::pair<const float*, size_t>>> taps;
 };
 
@@ -579,6 +583,24 @@ void Run::tap(const std::string& name, const float* p, size_t count) {
 // Mid-ResBlock activation emitted as fp16 hi/lo planes for the split GEMM.
 static bool split_a_enabled() { return true; }
 
+// A/B knob (DMX_CAT_PLANES=0): Up's concatenated input also written as f16 planes for conv1.
+static bool cat_planes_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("DMX_CAT_PLANES");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
+// A/B knob (DMX_PP=0): the 512-thread ping-pong kernel for large f16-plane convs.
+static bool pp_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("DMX_PP");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 // Implicit GEMM: conv3x3 (taps 9), ConvT phases (taps 4, phases 4), conv4x4-s2 (taps 16),
 // linear (taps 1).  Sources are plain NHWC (or the NCHW network input); grids too small to
 // fill the 256 CUs are split along K into deterministic slabs reduced by splitk_reduce_kernel
@@ -603,7 +625,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   const bool x3 = R.m->prec >= 1 && src_mode == SRC_PLAIN && cw.Bh != nullptr;
   const bool x1 = x3 && R.m->prec == 2;  // config-4 fp16: one MFMA on the hi planes
   // 512-thread ping-pong kernel (256-row tiles) for the large f16-plane convs
-  const bool pp = x3 && epi == EPI_STATS && cw.phases == 1 && s.C >= 32 && ash != nullptr &&
+  const bool pp = pp_enabled() && x3 && epi == EPI_STATS && cw.phases == 1 && s.C >= 32 && ash != nullptr &&
                   cdiv(M, 256) * cdiv(cw.cout, bn) >= 256;
   const int bk = pp ? 32 : x3 ? 64 : IG_BK;
   const int nkt = cw.kpad / bk;
@@ -753,29 +775,55 @@ static void norm(Run& R, NormParams np, int N) {
 
 // Split-K slabs of a deferred GEMM -> GroupNorm(1, C) application (reduce_norm_kernel): one
 // block per source sample; np describes the normalisation exactly as for norm().
+// Multi-block variant (reduce_norm_mb_kernel) from this many float4 per 1024 threads (A/B knob
+// DMX_RN_MB_KV; 0 = never).
+static int rn_mb_kv() {
+  static const int v = [] {
+    const char* e = std::getenv("DMX_RN_MB_KV");
+    return e ? std::atoi(e) : 4;
+  }();
+  return v;
+}
+
 static void reduce_norm(Run& R, const Deferred& d, NormParams np, int n_src_samples) {
-  if (R.plan) return;
-  const int n_out = np.n_src > 0 ? 2 * n_src_samples : n_src_samples;
   const int kv = cdiv(np.HW * (np.C / 4), 1024);
+  const bool mb = rn_mb_kv() > 0 && kv >= rn_mb_kv();
+  if (R.plan) {
+    if (mb) R.m->rn_need = std::max(R.m->rn_need, n_src_samples);
+    return;
+  }
+  const int n_out = np.n_src > 0 ? 2 * n_src_samples : n_src_samples;
   const int kvt = kv <= 1 ? 1 : kv <= 2 ? 2 : kv <= 4 ? 4 : RN_MAXV;
-  R.begin("reduce_norm_kernel<" + std::to_string(kvt) + ">", 0.0,
-          4.0 * (double)n_src_samples * np.HW * np.C * (d.splits + (np.res ? 1 : 0)) +
-              4.0 * (double)n_out * np.HW * np.C * (np.out_h ? 1 : 1));
-  if (kv <= 1) reduce_norm_kernel<1><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
-  else if (kv <= 2) reduce_norm_kernel<2><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
-  else if (kv <= 4) reduce_norm_kernel<4><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
-  else reduce_norm_kernel<RN_MAXV><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
+  const double bytes = 4.0 * (double)n_src_samples * np.HW * np.C * (d.splits + (np.res ? 1 : 0)) +
+                       4.0 * (double)n_out * np.HW * np.C;
+  if (mb) {
+    if (n_src_samples > R.m->rn_cap) throw Error(DMX_E_INTERNAL, "reduce_norm: hand-off state not sized");
+    R.begin("reduce_norm_mb_kernel<" + std::to_string(kvt) + ">", 0.0, bytes);
+    const dim3 grid(RN_NB, n_src_samples);
+    const RnSync sy = R.m->rn;
+    if (kv <= 1) reduce_norm_mb_kernel<1><<<grid, 256, 0, R.st>>>(d.partial, d.splits, d.bias, np, sy);
+    else if (kv <= 2) reduce_norm_mb_kernel<2><<<grid, 256, 0, R.st>>>(d.partial, d.splits, d.bias, np, sy);
+    else if (kv <= 4) reduce_norm_mb_kernel<4><<<grid, 256, 0, R.st>>>(d.partial, d.splits, d.bias, np, sy);
+    else reduce_norm_mb_kernel<RN_MAXV><<<grid, 256, 0, R.st>>>(d.partial, d.splits, d.bias, np, sy);
+  } else {
+    R.begin("reduce_norm_kernel<" + std::to_string(kvt) + ">", 0.0, bytes);
+    if (kv <= 1) reduce_norm_kernel<1><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
+    else if (kv <= 2) reduce_norm_kernel<2><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
+    else if (kv <= 4) reduce_norm_kernel<4><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
+    else reduce_norm_kernel<RN_MAXV><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
+  }
   R.end();
   HIPCHK(hipGetLastError());
 }
 
 template <int SRC>
-static void prep(Run& R, const SrcDesc& s, float* out, int N, int H, int W, const char* name) {
+static void prep(Run& R, const SrcDesc& s, float* out, int N, int H, int W, const char* name, _Float16* oh = nullptr,
+                 _Float16* ol = nullptr) {
   if (R.plan) return;
   const size_t total = (size_t)N * H * W * (s.C / 4);
   const int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
-  R.begin(name, 0.0, 4.0 * (double)N * H * W * s.C * (SRC == SRC_MAXPOOL ? 5 : 2));
-  prep_kernel<SRC><<<blocks, 256, 0, R.st>>>(s, out, N, H, W);
+  R.begin(name, 0.0, 4.0 * (double)N * H * W * s.C * (SRC == SRC_MAXPOOL ? 5 : 2) * (oh ? 1.5 : 1.0));
+  prep_kernel<SRC><<<blocks, 256, 0, R.st>>>(s, out, N, H, W, oh, ol);
   R.end();
   HIPCHK(hipGetLastError());
 }
@@ -1077,11 +1125,15 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
     const int nh = ch / 2, nw = cw / 2;
     const int nb = i == 0 ? S : N;  // samples computed in this stage before the emb add
     R.layer = "down" + std::to_string(i + 1) + ".0";
-    float* pooled = R.ws.get<float>((size_t)nb * nh * nw * cc);
-    prep<SRC_MAXPOOL>(R, mp, pooled, nb, nh, nw, "prep_kernel<2>");
+    const size_t pool_el = (size_t)nb * nh * nw * cc;
+    float* pooled = R.ws.get<float>(pool_el);
+    const bool pool_planes = R.m->prec >= 1 && m->down[i].r0.c1.Bh != nullptr && !R.m->debug && cat_planes_enabled();
+    _Float16* pool_h = pool_planes ? R.ws.get<_Float16>(2 * pool_el) : nullptr;
+    _Float16* pool_l = pool_planes ? pool_h + pool_el : nullptr;
+    prep<SRC_MAXPOOL>(R, mp, pooled, nb, nh, nw, "prep_kernel<2>", pool_h, pool_l);
     bool hp = false;
     float* h0 = resblock(R, m->down[i].r0, plain_src(pooled, cc), SRC_PLAIN, nb, nh, nw, true, nullptr, 0, 0, 0,
-                         nullptr, nullptr, m->down[i].r1.c1.Bh != nullptr, &hp);
+                         pool_h, pool_l, m->down[i].r1.c1.Bh != nullptr, &hp);
     R.layer = "down" + std::to_string(i + 1) + ".1";
     const _Float16* h0h = hp ? reinterpret_cast<const _Float16*>(h0) : nullptr;
     float* h1 = resblock(R, m->down[i].r1, plain_src(h0, cc), SRC_PLAIN, nb, nh, nw, false, emb, m->hsum,
@@ -1118,11 +1170,16 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
     u.padL = dx > 0 ? dx / 2 : 0;
     REQUIRE(u.C == m->up[i].r0.cin, "up: channel mismatch");
     R.layer = "up" + std::to_string(i + 1) + ".0";
-    float* cat = R.ws.get<float>((size_t)N * sh[si] * sw[si] * u.C);
-    prep<SRC_UPCAT>(R, u, cat, N, sh[si], sw[si], "prep_kernel<3>");
+    const size_t cat_el = (size_t)N * sh[si] * sw[si] * u.C;
+    float* cat = R.ws.get<float>(cat_el);
+    // the concat feeds conv1 (split GEMM: also as f16 planes) and the residual (fp32)
+    const bool cat_planes = R.m->prec >= 1 && m->up[i].r0.c1.Bh != nullptr && !R.m->debug && cat_planes_enabled();
+    _Float16* cat_h = cat_planes ? R.ws.get<_Float16>(2 * cat_el) : nullptr;
+    _Float16* cat_l = cat_planes ? cat_h + cat_el : nullptr;
+    prep<SRC_UPCAT>(R, u, cat, N, sh[si], sw[si], "prep_kernel<3>", cat_h, cat_l);
     bool hp = false;
     float* h0 = resblock(R, m->up[i].r0, plain_src(cat, u.C), SRC_PLAIN, N, sh[si], sw[si], true, nullptr, 0, 0, 0,
-                         nullptr, nullptr, m->up[i].r1.c1.Bh != nullptr, &hp);
+                         cat_h, cat_l, m->up[i].r1.c1.Bh != nullptr, &hp);
     R.layer = "up" + std::to_string(i + 1) + ".1";
     const _Float16* h0h = hp ? reinterpret_cast<const _Float16*>(h0) : nullptr;
     float* h1 = resblock(R, m->up[i].r1, plain_src(h0, u.C), SRC_PLAIN, N, sh[si], sw[si], false, emb, m->hsum,
@@ -1145,7 +1202,31 @@ static void check_shapes(dmx_model* m, int n, int h, int w) {
   REQUIRE(m->ctx->pos_table != nullptr, "time table not set (dmx_set_time_table)");
 }
 
+static void drop_graph(dmx_model* m) {
+  if (m->has_graph) {
+    (void)hipGraphExecDestroy(m->gexec);
+    (void)hipGraphDestroy(m->graph);
+    m->has_graph = false;
+  }
+}
+
+// reduce_norm_mb_kernel's hand-off state for the largest batch planned so far (zeroed: the
+// kernel leaves every counter at zero when it exits).
+static void ensure_rn(dmx_model* m) {
+  if (m->rn_need <= m->rn_cap) return;
+  drop_graph(m);  // captured launches hold the old pointers
+  if (m->rn.part) (void)hipFree(m->rn.part);
+  if (m->rn.cnt) (void)hipFree(m->rn.cnt);
+  const int cap = std::max(m->rn_need, 256);
+  HIPCHK(hipMalloc(&m->rn.part, (size_t)cap * RN_NB * 2 * sizeof(double)));
+  HIPCHK(hipMalloc(&m->rn.cnt, (size_t)cap * 2 * sizeof(unsigned) + 256));
+  HIPCHK(hipMemset(m->rn.cnt, 0, (size_t)cap * 2 * sizeof(unsigned) + 256));
+  m->rn.err = reinterpret_cast<int*>(m->rn.cnt + 2 * cap);
+  m->rn_cap = cap;
+}
+
 static void ensure_ws(dmx_model* m) {
+  ensure_rn(m);
   if (m->ws.off > m->ws_cap) {
     if (m->ws_mem) HIPCHK(hipFree(m->ws_mem));
     m->ws_mem = nullptr;
@@ -1469,6 +1550,8 @@ int dmx_model_destroy(dmx_model* m) {
     }
     for (void* p : m->owned) (void)hipFree(p);
     if (m->ws_mem) (void)hipFree(m->ws_mem);
+    if (m->rn.part) (void)hipFree(m->rn.part);
+    if (m->rn.cnt) (void)hipFree(m->rn.cnt);
     delete m;
   });
 }
@@ -1739,6 +1822,18 @@ int dmx_latent_frames_u8(const float* z, uint8_t* out, int n, int c, int h, int 
     REQUIRE(z && out, "null tensor");
     REQUIRE(n >= 1 && c >= 1 && h >= 1 && w >= 1, "bad shape");
     latent_frames_kernel<<<n * c, 256, 0, (hipStream_t)stream>>>(z, out, h * w);
+    HIPCHK(hipGetLastError());
+  });
+}
+
+int dmx_eval_metrics(const uint8_t* gt, const uint8_t* pred, int n, int h, int w, int gray, int threshold, int invert,
+                     double sigma, int* workspace, double* out, void* stream) {
+  return guarded([&] {
+    REQUIRE(gt && pred && workspace && out, "null tensor");
+    REQUIRE(n >= 1 && h >= 1 && w >= 1 && w <= 1024, "bad shape (1 <= w <= 1024)");
+    REQUIRE((size_t)h * w < ((size_t)1 << 31) && (size_t)h * h + (size_t)w * w < ((size_t)1 << 30), "image too large");
+    EvalParams p{gt, pred, h, w, gray, threshold, invert, sigma, workspace, out};
+    eval_metrics_kernel<<<n, 256, 0, (hipStream_t)stream>>>(p);
     HIPCHK(hipGetLastError());
   });
 }

@@ -152,6 +152,15 @@ int dmx_vae_decode(dmx_model* m, const float* z, float* img, uint8_t* u8, int n,
  * z: (n,c,h,w) fp32 device; out: (n,c,h,w) uint8 device, byte-identical to the reference's. */
 int dmx_latent_frames_u8(const float* z, uint8_t* out, int n, int c, int h, int w, void* stream);
 
+/* ---- generated-image metrics (replaces eval_iou_noise.py:77-94 binarisation and 162-272
+ * distance transform / compute_metrics) ------------------------------
+ * gt, pred: (n,h,w) uint8 device — masks (0 / nonzero; gray = 0) or grayscale images binarised
+ * here (gray = 1: foreground = v < threshold if invert else v >= threshold); w <= 1024.
+ * workspace: n*h*w int32 device scratch; out: (n,9) float64 device =
+ * {iou, gt_iou, far_noise_ratio, gauss_recall, inter, union, gt_area, pred_area, fp}. */
+int dmx_eval_metrics(const uint8_t* gt, const uint8_t* pred, int n, int h, int w, int gray, int threshold, int invert,
+                     double sigma, int* workspace, double* out, void* stream);
+
 /* ---- VAE encode (replaces VAE.encode, vae.py:51-62) -------------
  * x: (n,3,h,w) fp32, h and w multiples of 8; eps: (n,4,h/8,w/8) = the reference's
  * torch.randn_like(std) draw (caller-drawn, so the global RNG stream matches);

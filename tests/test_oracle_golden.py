@@ -134,3 +134,29 @@ def test_vae_forward_composes_encode_decode(golden, vae_sd):
         assert float(kl) == float(g["kl64"])
         assert torch.equal(x_recon, ref.vae_decode(vae_sd, z))
         assert float(loss) == float(((x_recon - x) ** 2).mean() + 1e-6 * kl)
+
+
+# ---- eval_iou_noise metrics: oracle vs the reference's outputs --------
+def test_eval_oracle_matches_reference_metrics(golden):
+    import numpy as np
+    from oracle import eval_ref
+    g = golden("eval_metrics.npz")
+    for i in range(g["metrics"].shape[0]):
+        gm, qm = eval_ref.binarize(g["gray_gt"][i]), eval_ref.binarize(g["gray_gen"][i])
+        assert np.array_equal(gm, g["mask_gt"][i]) and np.array_equal(qm, g["mask_gen"][i])
+        m = eval_ref.compute_metrics(gm, qm, 2.0)
+        got = np.array([m[k] for k in ("iou", "gt_iou", "far_noise_ratio", "gauss_recall", "inter", "union",
+                                       "gt_area", "pred_area", "fp")])
+        assert np.array_equal(got, g["metrics"][i]), i
+    m = eval_ref.compute_metrics(g["ns_gt"], g["ns_gen"], 3.5)
+    assert np.array_equal(np.array(list(m.values())), g["ns_metrics"])
+
+
+def test_eval_oracle_empty_gt_distance_convention():
+    """scipy's transform of an image with no GT pixel measures from the virtual feature (-1, 0):
+    the convention the native kernel reproduces (csrc/eval.h)."""
+    import numpy as np
+    from oracle import eval_ref
+    gt = np.zeros((5, 9), bool)
+    y, x = np.mgrid[0:5, 0:9]
+    assert np.array_equal(eval_ref.distance_map_to_gt(gt), np.sqrt(((y + 1) ** 2 + x ** 2).astype(np.float64)))
