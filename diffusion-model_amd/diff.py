@@ -21,7 +21,9 @@ What changes is where the work happens:
 from __future__ import annotations
 
 import os
+import queue
 import sys
+import threading
 from typing import Dict, Iterable, List, Optional, Tuple, Union
 
 import numpy as np
@@ -41,6 +43,54 @@ CLASS_KEYS = {1: ["x1", "y1", "x2", "y2"], 2: ["cx", "cy", "cr"], 3: ["ax", "ay"
 def _native_kind(model) -> int:
     """libdmx kind of a dmx drop-in network, 0 for foreign (duck-typed) models."""
     return int(getattr(type(model), "_dmx_kind", 0)) if hasattr(model, "native") else 0
+
+
+class _NoisePrefetch:
+    """The next `n` per-step noise draws of a sampler chunk, made on a helper thread from the
+    global CPU generator — in the reference's order, nothing else draws meanwhile — into pinned
+    buffers, so the host draw (~2 ms at B=64, single-threaded in torch) overlaps the GPU step
+    instead of preceding it.  torch.randn(shape, out=buf) consumes the generator exactly like
+    torch.randn(shape)."""
+
+    def __init__(self, shape, n: int, depth: int = 2):
+        self.shape, self.n = tuple(int(v) for v in shape), int(n)
+        self.bufs = [torch.empty(self.shape, pin_memory=True) for _ in range(depth + 2)]
+        self.events = [None] * len(self.bufs)
+        self.q: "queue.Queue" = queue.Queue(maxsize=depth)
+        self.err = None
+        self.thread = threading.Thread(target=self._run, daemon=True)
+        self.thread.start()
+
+    def _run(self):
+        try:
+            for k in range(self.n):
+                j = k % len(self.bufs)
+                if self.events[j] is not None:
+                    self.events[j].synchronize()  # the H2D copy that last read this buffer is done
+                torch.randn(self.shape, out=self.bufs[j])
+                self.q.put(k)
+        except BaseException as e:  # surfaced to the consumer
+            self.err = e
+            self.q.put(-1)
+
+    def next(self, device):
+        k = self.q.get()
+        if k < 0:
+            raise self.err
+        j = k % len(self.bufs)
+        out = self.bufs[j].to(device, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+        self.events[j] = ev
+        return out
+
+    def close(self):
+        while self.thread.is_alive():  # the consumer stopped early: let the producer finish its draws
+            try:
+                self.q.get(timeout=0.05)
+            except queue.Empty:
+                pass
+        self.thread.join()
 
 
 class Diffuser:
@@ -112,6 +162,9 @@ class Diffuser:
 
     def _step_noise(self, x):
         if self.noise_source == "host":
+            pf = self.__dict__.get("_prefetch")
+            if pf is not None and x.is_cuda and tuple(x.shape) == pf.shape:
+                return pf.next(x.device)
             return self._randn(x.shape, x.device)
         return None
 
@@ -159,7 +212,12 @@ class Diffuser:
     def denoise_cond(self, model, x, t, y=None, guidance_scale=0.0, null_label=0, cond_vals=None, cond_mask=None):
         """One DDPM step with optional classifier-free guidance (diff.py:127-162)."""
         T = self.num_timesteps
-        assert (t >= 1).all() and (t <= T).all()
+        assert (t >= 1).all() and (t <= T).all()  # (reads t back: a device sync, as in the reference)
+        return self._denoise_cond(model, x, t, y, guidance_scale, null_label, cond_vals, cond_mask)
+
+    def _denoise_cond(self, model, x, t, y=None, guidance_scale=0.0, null_label=0, cond_vals=None, cond_mask=None):
+        """denoise_cond after the range check — the samplers' own loops build t from a host-known
+        step in [1, T] and call this directly, so the host never waits on the device per step."""
         tables = self.coef_tables(x.device, clamp_prev=True)
         with torch.no_grad():
             if guidance_scale and y is not None and guidance_scale > 0:
@@ -240,21 +298,32 @@ class Diffuser:
         draws — in exact-fp32 MFMA mode.  `run(i_from, i_to, x)` advances t = i_from .. i_to + 1."""
         T = self.num_timesteps
         nm = self._guard_target(model) if x.is_cuda else None
+        prefetch = x.is_cuda and self.noise_source == "host" and _native_kind(model) != 0
         i = T
         while i >= 1:
             j = max(i - self.GUARD_CHUNK, 0)
             x0, rng = x, torch.get_rng_state()
-            x = run(i, j, x)
+            x = self._run_chunk(run, i, j, x, prefetch)
             if nm is not None and nm.range_tripped():
                 if on_replay is not None:
                     on_replay()
                 torch.set_rng_state(rng)
                 with nm.precision_override("fp32"):
-                    x = run(i, j, x0)
+                    x = self._run_chunk(run, i, j, x0, prefetch)
                 nm.range_tripped()  # clear
                 self.range_fallbacks += 1
             i = j
         return x
+
+    def _run_chunk(self, run, i, j, x, prefetch):
+        if not prefetch:
+            return run(i, j, x)
+        self._prefetch = _NoisePrefetch(x.shape, i - j)
+        try:
+            return run(i, j, x)
+        finally:
+            pf, self._prefetch = self._prefetch, None
+            pf.close()
 
     def sample_cond(self, model, x_shape, y, guidance_scale=0.0, null_label=0):
         """diff.py:165-172."""
@@ -449,10 +518,9 @@ class Diffuser:
             return x
 
         def run(i_from, i_to, x):
-            for i in range(i_from, i_to, -1):
+            for i in range(i_from, i_to, -1):  # i in [1, T]: denoise_cond's assert holds by construction
                 t = torch.full((x.shape[0],), i, device=x.device, dtype=torch.long)
-                x = self.denoise_cond(model=model, x=x, t=t, y=y, guidance_scale=guidance_scale,
-                                      null_label=null_label, cond_vals=vals, cond_mask=msk)
+                x = self._denoise_cond(model, x, t, y, guidance_scale, null_label, vals, msk)
                 if bar is not None:
                     bar.update(1)
             return x

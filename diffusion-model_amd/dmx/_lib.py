@@ -85,6 +85,9 @@ SIGNATURES = [
     ("dmx_model_destroy", _I, [_P]),
     ("dmx_model_set_tensor", _I, [_P, ctypes.c_char_p, _P, ctypes.POINTER(_I64), _I]),
     ("dmx_model_finalize", _I, [_P, _P]),
+    ("dmx_model_refresh", _I, [_P, _P]),
+    ("dmx_train_forward", _I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P, ctypes.POINTER(_I64), _P]),
+    ("dmx_train_backward", _I, [_P, _I64, _P, _P, ctypes.POINTER(_P), _I, _P]),
     ("dmx_model_set_precision", _I, [_P, _I]),
     ("dmx_model_get_precision", _I, [_P]),
     ("dmx_model_range_check", _I, [_P, _I, ctypes.POINTER(_I), _P]),

@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <stdexcept>
@@ -20,6 +21,7 @@
 #include "launch.h"
 #include "tokmlp.h"
 #include "eval.h"
+#include "train.h"
 
 namespace dmx {
 
@@ -188,11 +190,16 @@ struct ResW {
   ConvW c1, c2;
   Vec g1, b1, g2, b2;
   int cin = 0, mid = 0, cout = 0;
+  int cin_real = 0;     // channels of the reference tensor (cin is padded to a multiple of 4)
+  std::string prefix;   // state_dict prefix ("down1.maxpool_conv.1")
+  ConvW d1, d2;         // training: data-gradient GEMMs (flipped, transposed kernels; train.h)
 };
 struct AttnW {
   ConvW qkv, o, f1, f2;
   Vec l1w, l1b, l2w, l2b;
   int c = 0;
+  std::string prefix;
+  ConvW dqkv, dout, df1, df2;  // training: transposed Linear weights (data gradients)
 };
 struct DownUpW {
   ResW r0, r1;
@@ -218,6 +225,8 @@ struct GraphKey {
   int table_gen;  // dmx_ctx::table_gen at capture
   bool operator==(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(GraphKey)) == 0; }
 };
+
+struct Tape;  // training forward record (train_engine.h)
 
 }  // namespace dmx
 
@@ -265,10 +274,22 @@ struct dmx_model {
   bool debug = false;
   int prec = 1;  // 0: fp32 MFMA (exact fp32 products), 1: fp16 hi/lo x3 split MFMA, 2: fp16 (config 4)
   int* range_flag = nullptr;  // device int: an output went non-finite (kernels.h flag_nonfinite)
-  // reduce_norm_mb_kernel hand-off state (partials + counters per source sample), grown on demand
-  dmx::RnSync rn{};
-  int rn_cap = 0, rn_need = 0;
+
   std::vector<std::pair<std::string, std::pair<const float*, size_t>>> taps;
+  // Weight packing replay (dmx_model_refresh): every device-side repack / copy of the caller's
+  // tensors, in finalize order; the f16 planes of the split GEMMs are re-derived lazily
+  // (planes_stale) before the next split-precision launch.
+  std::vector<std::function<void(hipStream_t)>> jobs;
+  bool planes_stale = false;
+  unsigned* amax = nullptr;  // absmax scratch of split_planes
+  // training (train_engine.h): tape of the last dmx_train_forward, its workspace and the
+  // backward pass's workspace
+  bool train_ready = false;
+  dmx::Tape* tape = nullptr;
+  dmx::Arena tws, bws;
+  void *tws_mem = nullptr, *bws_mem = nullptr;
+  size_t tws_cap = 0, bws_cap = 0;
+  int64_t tape_id = 0;
 };
 
 namespace dmx {
@@ -276,6 +297,52 @@ namespace dmx {
 // ---------------------------------------------------------------------------
 // weight packing helpers (device-side repack of the caller's tensors)
 // ---------------------------------------------------------------------------
+// fp16 hi/lo planes of a packed fp32 B into c.Bh / c.Bl, scaled by 2^e so that
+// max|w| * 2^e ~ 2^13 (one host read of the absmax).
+static void split_planes(ConvW& c, hipStream_t st, unsigned* slot) {
+  const size_t n = (size_t)c.phases * c.npad * c.kpad;
+  HIPCHK(hipMemsetAsync(slot, 0, sizeof(unsigned), st));
+  absmax_kernel<<<256, 256, 0, st>>>(c.B, n, slot);
+  HIPCHK(hipGetLastError());
+  unsigned bits = 0;
+  HIPCHK(hipMemcpyAsync(&bits, slot, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  float mx;
+  std::memcpy(&mx, &bits, sizeof(float));
+  int e = 0;
+  if (mx > 0.f && std::isfinite(mx)) e = std::max(-8, std::min(24, (int)std::floor(std::log2(8192.0f / mx))));
+  const float scale = std::ldexp(1.0f, e);
+  c.inv_scale = std::ldexp(1.0f, -e);
+  split_weights_kernel<<<(int)std::min<size_t>((n + 255) / 256, 8192), 256, 0, st>>>(c.B, c.Bh, c.Bl, n, scale);
+  HIPCHK(hipGetLastError());
+}
+
+// Every split-GEMM weight of the model (the f16 planes are re-derived after a refresh).
+template <typename F>
+static void for_each_conv(dmx_model* m, F&& f) {
+  auto res = [&](ResW& r) {
+    f(r.c1);
+    f(r.c2);
+  };
+  res(m->inc);
+  for (int i = 0; i < 3; ++i) {
+    res(m->down[i].r0);
+    res(m->down[i].r1);
+    res(m->up[i].r0);
+    res(m->up[i].r1);
+    res(m->bot[i]);
+  }
+  for (auto& a : m->sa) {
+    f(a.qkv);
+    f(a.o);
+    f(a.f1);
+    f(a.f2);
+  }
+  for (auto& c : m->vconv) f(c);
+  for (auto& c : m->vconvt) f(c);
+  for (auto& c : m->venc) f(c);
+}
+
 struct Packer {
   dmx_model* m;
   hipStream_t st;
@@ -290,33 +357,24 @@ struct Packer {
     m->owned.push_back(p);
     return static_cast<float*>(p);
   }
+  // Run a packing step now and record it for dmx_model_refresh.
+  void job(std::function<void(hipStream_t)> f) {
+    f(st);
+    m->jobs.push_back(std::move(f));
+  }
   float* copy(const std::string& name) {
     auto& t = in(name);
     size_t n = 1;
     for (auto s : t.second) n *= (size_t)s;
     float* d = alloc(n);
-    HIPCHK(hipMemcpyAsync(d, t.first, n * sizeof(float), hipMemcpyDeviceToDevice, st));
+    const float* src = t.first;
+    job([=](hipStream_t s) { HIPCHK(hipMemcpyAsync(d, src, n * sizeof(float), hipMemcpyDeviceToDevice, s)); });
     return d;
   }
   Vec vec(const std::string& name) { return Vec{copy(name)}; }
-  // fp16 hi/lo planes of a packed fp32 B, scaled by 2^e so that max|w| * 2^e ~ 2^13
+  // fp16 hi/lo planes of a packed fp32 B (split_planes below)
   void split(ConvW& c) {
     const size_t n = (size_t)c.phases * c.npad * c.kpad;
-    unsigned* d = nullptr;
-    HIPCHK(hipMalloc(&d, sizeof(unsigned)));
-    m->owned.push_back(d);
-    HIPCHK(hipMemsetAsync(d, 0, sizeof(unsigned), st));
-    absmax_kernel<<<256, 256, 0, st>>>(c.B, n, d);
-    HIPCHK(hipGetLastError());
-    unsigned bits = 0;
-    HIPCHK(hipMemcpyAsync(&bits, d, sizeof(unsigned), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    float mx;
-    std::memcpy(&mx, &bits, sizeof(float));
-    int e = 0;
-    if (mx > 0.f && std::isfinite(mx)) e = std::max(-8, std::min(24, (int)std::floor(std::log2(8192.0f / mx))));
-    const float scale = std::ldexp(1.0f, e);
-    c.inv_scale = std::ldexp(1.0f, -e);
     void* h = nullptr;
     void* l = nullptr;
     HIPCHK(hipMalloc(&h, n * sizeof(_Float16)));
@@ -325,14 +383,24 @@ struct Packer {
     m->owned.push_back(l);
     c.Bh = static_cast<_Float16*>(h);
     c.Bl = static_cast<_Float16*>(l);
-    split_weights_kernel<<<(int)std::min<size_t>((n + 255) / 256, 8192), 256, 0, st>>>(c.B, c.Bh, c.Bl, n, scale);
-    HIPCHK(hipGetLastError());
+    split_planes(c, st, absmax_slot());
+  }
+  unsigned* absmax_slot() {
+    if (m->amax == nullptr) {
+      void* d = nullptr;
+      HIPCHK(hipMalloc(&d, 256));
+      m->owned.push_back(d);
+      m->amax = static_cast<unsigned*>(d);
+    }
+    return m->amax;
   }
   void repack(float* dst, const float* src, int kind, int P, int npad, int kpad, int cout, int cin, int ks) {
-    const size_t total = (size_t)P * npad * kpad;
-    const int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
-    repack_kernel<<<blocks, 256, 0, st>>>(dst, src, kind, P, npad, kpad, cout, cin, ks);
-    HIPCHK(hipGetLastError());
+    job([=](hipStream_t s) {
+      const size_t total = (size_t)P * npad * kpad;
+      const int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
+      repack_kernel<<<blocks, 256, 0, s>>>(dst, src, kind, P, npad, kpad, cout, cin, ks);
+      HIPCHK(hipGetLastError());
+    });
   }
   // Conv2d [cout][cin][ks][ks]; channel-padded to cin_pad (in_ch=3 first layer)
   ConvW conv(const std::string& w, const std::string& b, int cin, int cout, int ks, int cin_pad = 0) {
@@ -349,10 +417,12 @@ struct Packer {
     } else {
       // pad input channels: repack into a temporary [cout][cin_pad][ks][ks] first
       float* tmp = alloc((size_t)cout * cin_pad * ks * ks);
-      HIPCHK(hipMemsetAsync(tmp, 0, (size_t)cout * cin_pad * ks * ks * sizeof(float), st));
-      for (int o = 0; o < cout; ++o)
-        HIPCHK(hipMemcpyAsync(tmp + (size_t)o * cin_pad * ks * ks, in(w).first + (size_t)o * cin * ks * ks,
-                              (size_t)cin * ks * ks * sizeof(float), hipMemcpyDeviceToDevice, st));
+      const float* src = in(w).first;
+      job([=](hipStream_t s) {  // [cout][cin][k][k] rows into [cout][cin_pad][k][k] (zero padded)
+        HIPCHK(hipMemsetAsync(tmp, 0, (size_t)cout * cin_pad * ks * ks * sizeof(float), s));
+        HIPCHK(hipMemcpy2DAsync(tmp, (size_t)cin_pad * ks * ks * sizeof(float), src, (size_t)cin * ks * ks * sizeof(float),
+                                (size_t)cin * ks * ks * sizeof(float), cout, hipMemcpyDeviceToDevice, s));
+      });
       repack(c.B, tmp, 0, 1, c.npad, c.kpad, cout, cin_pad, ks);
     }
     if (!b.empty()) c.bias = copy(b);
@@ -392,6 +462,8 @@ struct Packer {
     r.cin = cin_pad ? cin_pad : cin;
     r.mid = mid;
     r.cout = cout;
+    r.cin_real = cin;
+    r.prefix = p;
     r.c1 = conv(p + ".double_conv.0.weight", "", cin, mid, 3, cin_pad);
     r.g1 = vec(p + ".double_conv.1.weight");
     r.b1 = vec(p + ".double_conv.1.bias");
@@ -403,6 +475,7 @@ struct Packer {
   AttnW attn(const std::string& p, int c) {
     AttnW a;
     a.c = c;
+    a.prefix = p;
     a.qkv = linear(p + ".mha.in_proj_weight", p + ".mha.in_proj_bias", c, 3 * c);
     a.o = linear(p + ".mha.out_proj.weight", p + ".mha.out_proj.bias", c, c);
     a.l1w = vec(p + ".ln.weight");
@@ -415,8 +488,11 @@ struct Packer {
   }
   float* transposed(const std::string& name, int rows, int cols) {
     float* d = alloc((size_t)rows * cols);
-    transpose_kernel<<<std::min(cdiv(rows * cols, 256), 4096), 256, 0, st>>>(d, in(name).first, rows, cols);
-    HIPCHK(hipGetLastError());
+    const float* src = in(name).first;
+    job([=](hipStream_t s) {
+      transpose_kernel<<<std::min(cdiv(rows * cols, 256), 4096), 256, 0, s>>>(d, src, rows, cols);
+      HIPCHK(hipGetLastError());
+    });
     return d;
   }
 };
@@ -498,11 +574,15 @@ static void finalize_model(dmx_model* m, hipStream_t st) {
     int o = 0;
     for (int i = 0; i < 6; ++i) {
       float* tp = P.transposed(std::string(all[i]) + ".emb_layer.1.weight", hc[i], 256);  // [256][hc]
-      for (int r = 0; r < 256; ++r)
-        HIPCHK(hipMemcpyAsync(m->wht + (size_t)r * m->hsum + o, tp + (size_t)r * hc[i], hc[i] * sizeof(float),
-                              hipMemcpyDeviceToDevice, st));
-      HIPCHK(hipMemcpyAsync(m->bh + o, P.in(std::string(all[i]) + ".emb_layer.1.bias").first,
-                            hc[i] * sizeof(float), hipMemcpyDeviceToDevice, st));
+      float* wd = m->wht + o;
+      float* bd = m->bh + o;
+      const float* bs = P.in(std::string(all[i]) + ".emb_layer.1.bias").first;
+      const int hs = m->hsum, w = hc[i];
+      P.job([=](hipStream_t s) {
+        HIPCHK(hipMemcpy2DAsync(wd, (size_t)hs * sizeof(float), tp, (size_t)w * sizeof(float), (size_t)w * sizeof(float),
+                                256, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(bd, bs, w * sizeof(float), hipMemcpyDeviceToDevice, s));
+      });
       o += hc[i];
     }
     if (cond) {
@@ -529,7 +609,7 @@ static void finalize_model(dmx_model* m, hipStream_t st) {
     HIPCHK(hipMemsetAsync(f, 0, 256, st));
   }
   HIPCHK(hipStreamSynchronize(st));
-  m->inputs.clear();  // caller's tensors are no longer referenced
+  // the registered tensors stay referenced only by dmx_model_refresh / training (include/dmx.h)
   m->finalized = true;
 }
 
@@ -583,23 +663,13 @@ void Run::tap(const std::string& name, const float* p, size_t count) {
 // Mid-ResBlock activation emitted as fp16 hi/lo planes for the split GEMM.
 static bool split_a_enabled() { return true; }
 
-// A/B knob (DMX_CAT_PLANES=0): Up's concatenated input also written as f16 planes for conv1.
-static bool cat_planes_enabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("DMX_CAT_PLANES");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  return v;
-}
+// Max-pool / up-concat sources also written as f16 planes for the next conv1 (split GEMM A;
+// measured +0.2 %, same-box A/B) — they stay fp32 too, as the residual of that ResBlock.
+static bool cat_planes_enabled() { return true; }
 
-// A/B knob (DMX_PP=0): the 512-thread ping-pong kernel for large f16-plane convs.
-static bool pp_enabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("DMX_PP");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  return v;
-}
+// The 512-thread ping-pong kernel for the large f16-plane convs (measured +1.3 % over the
+// two-block kernel, same-box A/B).
+static bool pp_enabled() { return true; }
 
 // Implicit GEMM: conv3x3 (taps 9), ConvT phases (taps 4, phases 4), conv4x4-s2 (taps 16),
 // linear (taps 1).  Sources are plain NHWC (or the NCHW network input); grids too small to
@@ -775,43 +845,18 @@ static void norm(Run& R, NormParams np, int N) {
 
 // Split-K slabs of a deferred GEMM -> GroupNorm(1, C) application (reduce_norm_kernel): one
 // block per source sample; np describes the normalisation exactly as for norm().
-// Multi-block variant (reduce_norm_mb_kernel) from this many float4 per 1024 threads (A/B knob
-// DMX_RN_MB_KV; 0 = never).
-static int rn_mb_kv() {
-  static const int v = [] {
-    const char* e = std::getenv("DMX_RN_MB_KV");
-    return e ? std::atoi(e) : 4;
-  }();
-  return v;
-}
-
 static void reduce_norm(Run& R, const Deferred& d, NormParams np, int n_src_samples) {
+  if (R.plan) return;
   const int kv = cdiv(np.HW * (np.C / 4), 1024);
-  const bool mb = rn_mb_kv() > 0 && kv >= rn_mb_kv();
-  if (R.plan) {
-    if (mb) R.m->rn_need = std::max(R.m->rn_need, n_src_samples);
-    return;
-  }
   const int n_out = np.n_src > 0 ? 2 * n_src_samples : n_src_samples;
   const int kvt = kv <= 1 ? 1 : kv <= 2 ? 2 : kv <= 4 ? 4 : RN_MAXV;
-  const double bytes = 4.0 * (double)n_src_samples * np.HW * np.C * (d.splits + (np.res ? 1 : 0)) +
-                       4.0 * (double)n_out * np.HW * np.C;
-  if (mb) {
-    if (n_src_samples > R.m->rn_cap) throw Error(DMX_E_INTERNAL, "reduce_norm: hand-off state not sized");
-    R.begin("reduce_norm_mb_kernel<" + std::to_string(kvt) + ">", 0.0, bytes);
-    const dim3 grid(RN_NB, n_src_samples);
-    const RnSync sy = R.m->rn;
-    if (kv <= 1) reduce_norm_mb_kernel<1><<<grid, 256, 0, R.st>>>(d.partial, d.splits, d.bias, np, sy);
-    else if (kv <= 2) reduce_norm_mb_kernel<2><<<grid, 256, 0, R.st>>>(d.partial, d.splits, d.bias, np, sy);
-    else if (kv <= 4) reduce_norm_mb_kernel<4><<<grid, 256, 0, R.st>>>(d.partial, d.splits, d.bias, np, sy);
-    else reduce_norm_mb_kernel<RN_MAXV><<<grid, 256, 0, R.st>>>(d.partial, d.splits, d.bias, np, sy);
-  } else {
-    R.begin("reduce_norm_kernel<" + std::to_string(kvt) + ">", 0.0, bytes);
-    if (kv <= 1) reduce_norm_kernel<1><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
-    else if (kv <= 2) reduce_norm_kernel<2><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
-    else if (kv <= 4) reduce_norm_kernel<4><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
-    else reduce_norm_kernel<RN_MAXV><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
-  }
+  R.begin("reduce_norm_kernel<" + std::to_string(kvt) + ">", 0.0,
+          4.0 * (double)n_src_samples * np.HW * np.C * (d.splits + (np.res ? 1 : 0)) +
+              4.0 * (double)n_out * np.HW * np.C);
+  if (kv <= 1) reduce_norm_kernel<1><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
+  else if (kv <= 2) reduce_norm_kernel<2><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
+  else if (kv <= 4) reduce_norm_kernel<4><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
+  else reduce_norm_kernel<RN_MAXV><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
   R.end();
   HIPCHK(hipGetLastError());
 }
@@ -1210,23 +1255,18 @@ static void drop_graph(dmx_model* m) {
   }
 }
 
-// reduce_norm_mb_kernel's hand-off state for the largest batch planned so far (zeroed: the
-// kernel leaves every counter at zero when it exits).
-static void ensure_rn(dmx_model* m) {
-  if (m->rn_need <= m->rn_cap) return;
-  drop_graph(m);  // captured launches hold the old pointers
-  if (m->rn.part) (void)hipFree(m->rn.part);
-  if (m->rn.cnt) (void)hipFree(m->rn.cnt);
-  const int cap = std::max(m->rn_need, 256);
-  HIPCHK(hipMalloc(&m->rn.part, (size_t)cap * RN_NB * 2 * sizeof(double)));
-  HIPCHK(hipMalloc(&m->rn.cnt, (size_t)cap * 2 * sizeof(unsigned) + 256));
-  HIPCHK(hipMemset(m->rn.cnt, 0, (size_t)cap * 2 * sizeof(unsigned) + 256));
-  m->rn.err = reinterpret_cast<int*>(m->rn.cnt + 2 * cap);
-  m->rn_cap = cap;
+// Re-derive the f16 planes of the split GEMMs after dmx_model_refresh (weights changed in
+// place), before the next split-precision launch; captured graphs hold the old scales.
+static void ensure_planes(dmx_model* m, hipStream_t st) {
+  if (!m->planes_stale || m->prec < 1) return;
+  drop_graph(m);
+  for_each_conv(m, [&](ConvW& c) {
+    if (c.Bh != nullptr) split_planes(c, st, m->amax);
+  });
+  m->planes_stale = false;
 }
 
 static void ensure_ws(dmx_model* m) {
-  ensure_rn(m);
   if (m->ws.off > m->ws_cap) {
     if (m->ws_mem) HIPCHK(hipFree(m->ws_mem));
     m->ws_mem = nullptr;
@@ -1402,6 +1442,8 @@ static void vae_enc_body(Run& R, const float* x, const float* eps, float* z, flo
 
 }  // namespace dmx
 
+#include "train_engine.h"
+
 // ===========================================================================
 // C ABI
 // ===========================================================================
@@ -1550,8 +1592,9 @@ int dmx_model_destroy(dmx_model* m) {
     }
     for (void* p : m->owned) (void)hipFree(p);
     if (m->ws_mem) (void)hipFree(m->ws_mem);
-    if (m->rn.part) (void)hipFree(m->rn.part);
-    if (m->rn.cnt) (void)hipFree(m->rn.cnt);
+    if (m->tws_mem) (void)hipFree(m->tws_mem);
+    if (m->bws_mem) (void)hipFree(m->bws_mem);
+    delete m->tape;
     delete m;
   });
 }
@@ -1580,6 +1623,53 @@ int dmx_model_finalize(dmx_model* m, void* stream) {
 }
 
 int64_t dmx_model_workspace_bytes(const dmx_model* m) { return m ? (int64_t)m->ws_cap : -1; }
+
+int dmx_model_refresh(dmx_model* m, void* stream) {
+  return guarded([&] {
+    REQUIRE(m != nullptr, "null model");
+    refresh_model(m, (hipStream_t)stream);
+  });
+}
+
+int dmx_train_forward(dmx_model* m, const float* x, const int64_t* t, const int64_t* y, const float* vals,
+                      const float* mask, int n, int h, int w, float* eps, float* geom, int64_t* tape_id,
+                      void* stream) {
+  return guarded([&] {
+    REQUIRE(m != nullptr && tape_id != nullptr, "null argument");
+    check_train(m, n, h, w);
+    REQUIRE(x && t && y && eps, "null tensor");
+    REQUIRE((vals == nullptr) == (mask == nullptr), "vals and mask must be given together");
+    REQUIRE(geom == nullptr || m->kind == DMX_UNET_COND_GEOM, "geom output only for UnetCondWithGeomHead");
+    hipStream_t st = (hipStream_t)stream;
+    ensure_train(m, st);
+    if (m->tape == nullptr) m->tape = new Tape();
+    Tape& T = *m->tape;
+    T.id = 0;  // invalid until the forward below has been enqueued
+    TrainArgs a{x, t, y, vals, mask, n, h, w, eps, geom};
+    with_fp32(m, [&] {
+      run_arena(m, st, m->tws, m->tws_mem, m->tws_cap, [&](Run& R) { train_fwd_body(R, T, a); });
+    });
+    T.id = ++m->tape_id;
+    *tape_id = T.id;
+  });
+}
+
+int dmx_train_backward(dmx_model* m, int64_t tape_id, const float* d_eps, const float* d_geom, float* const* grads,
+                       int n_grads, void* stream) {
+  return guarded([&] {
+    REQUIRE(m != nullptr && grads != nullptr, "null argument");
+    REQUIRE(m->tape != nullptr && m->tape->id != 0, "no training forward recorded (dmx_train_forward)");
+    REQUIRE(tape_id == m->tape->id,
+            "stale tape: another dmx_train_forward ran after the one this backward belongs to");
+    REQUIRE(n_grads == (int)m->keys.size(), "grads must hold one pointer per state_dict key");
+    GradMap G;
+    for (int i = 0; i < n_grads; ++i) G.g[m->keys[i].name] = grads[i];
+    hipStream_t st = (hipStream_t)stream;
+    with_fp32(m, [&] {
+      run_arena(m, st, m->bws, m->bws_mem, m->bws_cap, [&](Run& R) { train_bwd_body(R, *m->tape, G, d_eps, d_geom); });
+    });
+  });
+}
 
 int dmx_model_set_precision(dmx_model* m, int prec) {
   return guarded([&] {
@@ -1642,6 +1732,7 @@ int dmx_unet_forward(dmx_model* m, const float* x, const int64_t* t, const int64
     REQUIRE((vals == nullptr) == (mask == nullptr), "vals and mask must be given together");
     REQUIRE(geom == nullptr || m->kind == DMX_UNET_COND_GEOM, "geom output only for UnetCondWithGeomHead");
     hipStream_t st = (hipStream_t)stream;
+    ensure_planes(m, st);
     m->taps.clear();
     run_planned(m, st, [&](Run& R) {
       FwdIn in{x, n, t, 1, y, 0, 0, vals, mask, n};
@@ -1663,6 +1754,7 @@ int dmx_step(dmx_model* m, const dmx_step_args* a, void* stream) {
   return guarded([&] {
     REQUIRE(m != nullptr, "null model");
     validate_step(m, a);
+    ensure_planes(m, (hipStream_t)stream);
     run_planned(m, (hipStream_t)stream, [&](Run& R) { step_body(R, *a); });
   });
 }
@@ -1676,6 +1768,7 @@ int dmx_sample_loop(dmx_model* m, const dmx_step_args* a, int steps, int use_gra
     REQUIRE(a->noise == nullptr, "sample loop draws on-device Philox noise (noise must be NULL)");
     REQUIRE(steps >= 0, "steps must be >= 0");
     hipStream_t st = (hipStream_t)stream;
+    ensure_planes(m, st);
     int64_t* tdev = const_cast<int64_t*>(a->t);
     if (!use_graph) {
       for (int i = 0; i < steps; ++i) {
@@ -1733,6 +1826,7 @@ int dmx_step_profile(dmx_model* m, const dmx_step_args* a, dmx_kernel_record* re
     REQUIRE(m != nullptr && recs != nullptr && n_out != nullptr, "null argument");
     validate_step(m, a);
     hipStream_t st = (hipStream_t)stream;
+    ensure_planes(m, st);
     Prof prof;
     m->ws.base = nullptr;
     m->ws.off = 0;
@@ -1807,6 +1901,7 @@ int dmx_vae_decode(dmx_model* m, const float* z, float* img, uint8_t* u8, int n,
     REQUIRE(n >= 1 && h >= 1 && w >= 1, "bad shape");
     const int chunk = 16;  // bounds workspace (the reference decodes in chunks of 4, diff.py:353)
     hipStream_t st = (hipStream_t)stream;
+    ensure_planes(m, st);
     for (int s = 0; s < n; s += chunk) {
       const int b = std::min(chunk, n - s);
       run_planned(m, st, [&](Run& R) {
@@ -1849,6 +1944,7 @@ int dmx_vae_encode(dmx_model* m, const float* x, const float* eps, float* z, flo
     const int chunk = 16;  // bounds workspace
     const int hl = h / 8, wl = w / 8;
     hipStream_t st = (hipStream_t)stream;
+    ensure_planes(m, st);
     for (int s = 0; s < n; s += chunk) {
       const int b = std::min(chunk, n - s);
       run_planned(m, st, [&](Run& R) {

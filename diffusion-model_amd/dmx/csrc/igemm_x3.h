@@ -541,236 +541,3 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 
 }  // namespace dmx
 
-namespace dmx {
-
-// ---------------------------------------------------------------------------
-// attention_x3_kernel with the chunk loop software-pipelined (D = 16, 32): while the wave runs
-// the online softmax of chunk c on the VALU, the S^T MFMAs of chunk c+1 are already issued,
-// so the matrix pipe and the VALU of one wave overlap instead of alternating (the D = 16 core is
-// VALU-heavy: exp2 + max + hi/lo split per score against 18 MFMAs per 64-key chunk).  K / V
-// chunks rotate through three LDS buffers so one barrier per chunk suffices: the buffer a
-// chunk is staged into was last read (by PV) two iterations earlier, behind the previous
-// barrier.  Same arithmetic, same summation order as attention_x3_kernel (results identical).
-// ---------------------------------------------------------------------------
-template <int D, int X1 = 0>
-__global__ __launch_bounds__(256) void attention_x3p_kernel(const float* qkv, float* out, int L, int C) {
-  constexpr int KC = 64, KS = D + 8, VR = 32, VS = KC + 4, NKS = D / 16, NB = 3;
-  static_assert(D == 16 || D == 32, "pipelined core: D in {16, 32}");
-  __shared__ __attribute__((aligned(16))) _Float16 Kh[NB][KC][KS];
-  __shared__ __attribute__((aligned(16))) _Float16 Kl[NB][X1 ? 1 : KC][KS];
-  __shared__ __attribute__((aligned(16))) _Float16 Vh[NB][VR][VS];
-  __shared__ __attribute__((aligned(16))) _Float16 Vl[NB][X1 ? 1 : VR][VS];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int hd = blockIdx.y, n = blockIdx.z;
-  const int fr = lane & 31, fh = lane >> 5;
-  const size_t rs = (size_t)3 * C;
-  const float* base = qkv + (size_t)n * L * rs;
-  const float qscale = 1.4426950408889634f / sqrtf((float)D);
-  const int q = blockIdx.x * 128 + wid * 32 + fr;
-
-  half8 qh[NKS], ql[NKS];
-#pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) {
-    floatx4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
-    if (q < L) {
-      const float* r = base + (size_t)q * rs + hd * D + 16 * ks + 8 * fh;
-      a = ld4(r);
-      b = ld4(r + 4);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float va = a[j] * qscale, vb = b[j] * qscale;
-      const _Float16 ha = (_Float16)va, hb = (_Float16)vb;
-      qh[ks][j] = ha;
-      ql[ks][j] = (_Float16)(va - (float)ha);
-      qh[ks][j + 4] = hb;
-      ql[ks][j + 4] = (_Float16)(vb - (float)hb);
-    }
-  }
-  constexpr bool ONES = VR > D;  // D = 16: V^T row D holds ones -> the MFMA sums the denominator
-  if constexpr (ONES) {
-    for (int i = tid; i < NB * (VR - D) * VS; i += 256) {
-      const int bb = i / ((VR - D) * VS), rem = i % ((VR - D) * VS), r = D + rem / VS;
-      Vh[bb][r][rem % VS] = (_Float16)(r == D ? 1.f : 0.f);
-      if constexpr (!X1) Vl[bb][r][rem % VS] = (_Float16)0.f;
-    }
-  }
-  floatx16 o;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) o[r] = 0.f;
-  float mrun = -INFINITY, lrun = 0.f;
-
-  constexpr int IT = KC * (D / 4) / 256;
-  static_assert(IT >= 1, "staging");
-  floatx4 kr[IT], vr[IT];
-  auto load_kv = [&](int c0) {
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int i = tid + 256 * it, key = i / (D / 4), d4 = (i % (D / 4)) * 4;
-      const float* r = base + (size_t)min(c0 + key, L - 1) * rs + hd * D + d4;
-      kr[it] = ld4(r + C);
-      vr[it] = ld4(r + 2 * C);
-    }
-  };
-  auto store_kv = [&](int bb, int c0) {
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int i = tid + 256 * it, key = i / (D / 4), d4 = (i % (D / 4)) * 4;
-      const bool kvalid = c0 + key < L;
-      const floatx4 z = {0.f, 0.f, 0.f, 0.f};
-      half4 h, l;
-      if constexpr (X1) {
-        *reinterpret_cast<half4*>(&Kh[bb][key][d4]) = __builtin_convertvector(kvalid ? kr[it] : z, half4);
-        h = __builtin_convertvector(kvalid ? vr[it] : z, half4);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) Vh[bb][d4 + j][key] = h[j];
-        continue;
-      }
-      split4(kvalid ? kr[it] : z, h, l);
-      *reinterpret_cast<half4*>(&Kh[bb][key][d4]) = h;
-      *reinterpret_cast<half4*>(&Kl[bb][key][d4]) = l;
-      split4(kvalid ? vr[it] : z, h, l);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        Vh[bb][d4 + j][key] = h[j];
-        Vl[bb][d4 + j][key] = l[j];
-      }
-    }
-  };
-  auto qk = [&](int bb, floatx16 (&sc)[2]) {
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sc[kt][r] = 0.f;
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        const half8 kh = *reinterpret_cast<const half8*>(&Kh[bb][kt * 32 + fr][16 * ks + 8 * fh]);
-        if constexpr (!X1) {
-          const half8 kl = *reinterpret_cast<const half8*>(&Kl[bb][kt * 32 + fr][16 * ks + 8 * fh]);
-          sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kl, qh[ks], sc[kt], 0, 0, 0);
-          sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, ql[ks], sc[kt], 0, 0, 0);
-        }
-        sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, qh[ks], sc[kt], 0, 0, 0);
-      }
-    }
-  };
-
-  const int nc = (L + KC - 1) / KC;
-  load_kv(0);
-  store_kv(0, 0);
-  if (nc > 1) load_kv(KC);
-  __syncthreads();
-  floatx16 sc[2];
-  qk(0, sc);
-  for (int c = 0; c < nc; ++c) {
-    const int c0 = c * KC, bb = c % NB;
-    if (c + 1 < nc) store_kv((c + 1) % NB, c0 + KC);  // buffer last read by PV two chunks ago
-    __syncthreads();
-    if (c + 2 < nc) load_kv(c0 + 2 * KC);  // in flight during this chunk's work
-    floatx16 sn[2];
-    if (c + 1 < nc) qk((c + 1) % NB, sn);  // next chunk's scores: independent of the softmax below
-    const int nvalid = L - c0;
-    if (nvalid < KC) {
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-          if (key >= nvalid) sc[kt][r] = -INFINITY;
-        }
-    }
-    float mx = sc[0][0];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kt][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float mnew = fmaxf(mrun, mx);
-    const float alpha = __builtin_amdgcn_exp2f(mrun - mnew);
-    mrun = mnew;
-    const f32x2 mn2 = {mnew, mnew}, al2 = {alpha, alpha};
-    f32x2 ls2 = {0.f, 0.f};
-    u32x4 phu[2][2], plu[2][2];
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int jp = 0; jp < 4; ++jp) {
-          f32x2 v = {sc[kt][8 * s + 2 * jp], sc[kt][8 * s + 2 * jp + 1]};
-          v -= mn2;
-          v.x = __builtin_amdgcn_exp2f(v.x);
-          v.y = __builtin_amdgcn_exp2f(v.y);
-          if constexpr (!ONES) ls2 += v;
-          unsigned h, l;
-          if constexpr (X1) {
-            h = __builtin_bit_cast(unsigned, __builtin_convertvector(v, half2v));
-            l = 0u;
-          } else {
-            split2(v, h, l);
-          }
-          phu[kt][s][jp] = h;
-          plu[kt][s][jp] = l;
-        }
-    if constexpr (!ONES) lrun = lrun * alpha + (ls2.x + ls2.y);
-#pragma unroll
-    for (int r = 0; r < 16; r += 2) {
-      f32x2 v = {o[r], o[r + 1]};
-      v *= al2;
-      o[r] = v.x;
-      o[r + 1] = v.y;
-    }
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const half8 ph = __builtin_bit_cast(half8, phu[kt][s]);
-        const half8 pl = __builtin_bit_cast(half8, plu[kt][s]);
-        const int k0 = kt * 32 + 16 * s + 4 * fh;
-        half8 vh, vl;
-        const half4 a0 = *reinterpret_cast<const half4*>(&Vh[bb][fr][k0]);
-        const half4 a1 = *reinterpret_cast<const half4*>(&Vh[bb][fr][k0 + 8]);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          vh[j] = a0[j];
-          vh[j + 4] = a1[j];
-        }
-        if constexpr (!X1) {
-          const half4 b0 = *reinterpret_cast<const half4*>(&Vl[bb][fr][k0]);
-          const half4 b1 = *reinterpret_cast<const half4*>(&Vl[bb][fr][k0 + 8]);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            vl[j] = b0[j];
-            vl[j + 4] = b1[j];
-          }
-          o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph, o, 0, 0, 0);
-          o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, pl, o, 0, 0, 0);
-        }
-        o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, o, 0, 0, 0);
-      }
-    if (c + 1 < nc) {
-      sc[0] = sn[0];
-      sc[1] = sn[1];
-    }
-  }
-  if constexpr (ONES) {
-    lrun = __shfl(o[8], fr, 64);
-  } else {
-    lrun += __shfl_xor(lrun, 32, 64);
-  }
-  const float inv = 1.0f / lrun;
-  if (q < L) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int d = 8 * g + 4 * fh;
-      if (d < D) {
-        floatx4 v;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = o[4 * g + j] * inv;
-        *reinterpret_cast<floatx4*>(out + ((size_t)n * L + q) * C + hd * D + d) = v;
-      }
-    }
-  }
-}
-
-}  // namespace dmx

@@ -373,154 +373,6 @@ __global__ __launch_bounds__(1024) void reduce_norm_kernel(const float* partial,
   }
 }
 
-// reduce_norm_kernel spread over RN_NB workgroups per source sample (grid = (RN_NB, samples),
-// 256 threads each): the sample's 1024 "threads" of reduce_norm_kernel become RN_NB blocks of
-// 256 (same element-to-thread map, so each holds 1/RN_NB of the sample in registers).  Each block
-// publishes its (sum, sum of squares) partial, the blocks of a sample meet at a per-sample counter
-// (cross-workgroup hand-off, MI355X_MICROARCH.md "Valid forms", row 1: write-through sc1 partial
-// stores drained by s_waitcnt vmcnt(0) before one agent-scope counter add; an sc1 poll by one lane,
-// a workgroup barrier, then sc1 loads of the partials), and every block sums the RN_NB partials in
-// block order — a fixed order, so the statistics are identical in every block and every run.  The
-// last block to leave resets the counters for the next launch.  The grid (<= 2 blocks per CU at
-// this model's sizes) is co-resident; the poll is bounded all the same (err flag, no hang).
-constexpr int RN_NB = 4;
-struct RnSync {
-  double* part;       // [samples][RN_NB][2]
-  unsigned* cnt;      // [samples][2]: arrived, departed
-  int* err;           // set when a poll gave up
-};
-
-DMX_DEV void st_sc1(double* p, double v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-DMX_DEV double ld_sc1(const double* p) {
-  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int KV>
-__global__ __launch_bounds__(256) void reduce_norm_mb_kernel(const float* partial, int splits, const float* bias,
-                                                             const NormParams p, const RnSync sy) {
-  constexpr int SB = KV >= 16 ? 1 : 16 / KV;  // slabs per batch
-  constexpr int NT = RN_NB * 256;             // "threads" per sample
-  const int b = blockIdx.x, s = blockIdx.y, tid = threadIdx.x, g = b * 256 + tid;
-  const int C4 = p.C >> 2, per = p.HW * C4;
-  const size_t sstride = (size_t)gridDim.y * per * 4;  // floats per split slab (all source samples)
-  const size_t sbase = (size_t)s * per * 4;
-  floatx4 v[KV];
-  float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-  for (int k = 0; k < KV; ++k) v[k] = floatx4{0.f, 0.f, 0.f, 0.f};
-  for (int sp0 = 0; sp0 < splits; sp0 += SB) {
-    floatx4 a[SB][KV];
-#pragma unroll
-    for (int q = 0; q < SB; ++q)
-#pragma unroll
-      for (int k = 0; k < KV; ++k) {
-        const int idx = g + NT * k;
-        a[q][k] = (sp0 + q < splits && idx < per) ? ld4(partial + (sp0 + q) * sstride + sbase + (size_t)idx * 4)
-                                                  : floatx4{0.f, 0.f, 0.f, 0.f};
-      }
-#pragma unroll
-    for (int q = 0; q < SB; ++q)
-#pragma unroll
-      for (int k = 0; k < KV; ++k)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[k][j] += a[q][k][j];
-  }
-#pragma unroll
-  for (int k = 0; k < KV; ++k) {
-    const int idx = g + NT * k;
-    if (idx < per) {
-      if (bias != nullptr) {
-        const floatx4 bb = ld4(bias + (idx % C4) * 4);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[k][j] += bb[j];
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        s1 += v[k][j];
-        s2 += v[k][j] * v[k][j];
-      }
-    }
-  }
-  __shared__ double r1[4], r2[4];
-  __shared__ float2 st_s;
-  double d1 = s1, d2 = s2;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    d1 += __shfl_xor(d1, o, 64);
-    d2 += __shfl_xor(d2, o, 64);
-  }
-  if ((tid & 63) == 0) {
-    r1[tid >> 6] = d1;
-    r2[tid >> 6] = d2;
-  }
-  __syncthreads();
-  unsigned* cnt = sy.cnt + 2 * s;
-  double* part = sy.part + (size_t)s * RN_NB * 2;
-  if (tid == 0) {
-    st_sc1(part + 2 * b, (r1[0] + r1[1]) + (r1[2] + r1[3]));
-    st_sc1(part + 2 * b + 1, (r2[0] + r2[1]) + (r2[2] + r2[3]));
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int spins = 0;
-    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)RN_NB) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1 << 22)) {  // never expected: the grid is co-resident
-        *sy.err = 1;
-        break;
-      }
-    }
-    double a1 = 0.0, a2 = 0.0;
-    for (int q = 0; q < RN_NB; ++q) {
-      a1 += ld_sc1(part + 2 * q);
-      a2 += ld_sc1(part + 2 * q + 1);
-    }
-    const double cntd = (double)p.HW * (double)p.C;
-    const double mean = a1 / cntd;
-    double var = a2 / cntd - mean * mean;
-    var = var < 0.0 ? 0.0 : var;
-    st_s = make_float2((float)mean, (float)(1.0 / sqrt(var + 1e-5)));
-    if (__hip_atomic_fetch_add(cnt + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)RN_NB - 1) {
-      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every block has read: reset
-      __hip_atomic_store(cnt + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-  const float2 st = st_s;
-  const int nout = p.n_src > 0 ? 2 : 1;
-  for (int q = 0; q < nout; ++q) {
-    const int n = s + q * (p.n_src > 0 ? p.n_src : 0);
-    const size_t base = (size_t)n * per * 4;
-#pragma unroll
-    for (int k = 0; k < KV; ++k) {
-      const int idx = g + NT * k;
-      if (idx >= per) break;
-      const int c = (idx % C4) * 4;
-      floatx4 o = gn_apply4(v[k], st, p.gamma, p.beta, c, 0);
-      if (p.res != nullptr) {
-        const floatx4 r = ld4(p.res + sbase + (size_t)idx * 4);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = gelu(r[j] + o[j]);
-      } else if (p.act) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = gelu(o[j]);
-      }
-      if (p.emb != nullptr) {
-        const floatx4 e = ld4(p.emb + (size_t)n * p.emb_stride + p.emb_off + c);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] += e[j];
-      }
-      const size_t off = base + (size_t)idx * 4;
-      if (p.out != nullptr) *reinterpret_cast<floatx4*>(p.out + off) = o;
-      if (p.out_h != nullptr) {
-        half4 hh, ll;
-        split4(o, hh, ll);
-        *reinterpret_cast<half4*>(p.out_h + off) = hh;
-        *reinterpret_cast<half4*>(p.out_l + off) = ll;
-      }
-    }
-  }
-}
-
 // Materialise a fused source (2x2 max-pool, bilinear-x2 + pad + concat) as a plain
 // NHWC tensor [N][H][W][C] (models/unet_cond.py:58, 88-97).
 // oh / ol (optional): the same values also as f16 hi / lo planes (the next conv's split-GEMM A).

@@ -1,0 +1,701 @@
+// dmx — backward kernels of the U-Net training step (train_latent_cond.py:136-163
+// forward / backward of UnetCondWithGeomHead, models/unet_cond.py + models/unet_cond_geom.py).
+//
+// Layout as the forward: activations NHWC fp32, GroupNorm(1, C) per sample, LayerNorm per token.
+// Every reduction runs in a fixed order (per-block partials, then a fixed-order sum), so a
+// backward pass is deterministic run to run.  Exact fp32 arithmetic throughout (the GEMM-shaped
+// parts run on the fp32 MFMA path: igemm_f32 for the data gradients, wgrad_kernel below for the
+// weight gradients).
+#pragma once
+#include "common.h"
+
+namespace dmx {
+
+DMX_DEV float gelu_grad(float x) {  // d/dx 0.5 x (1 + erf(x / sqrt 2)) = Phi(x) + x phi(x)
+  return 0.5f * (1.0f + erff(x * 0.70710678118654752440f)) + x * 0.39894228040143267794f * expf(-0.5f * x * x);
+}
+DMX_DEV float silu_grad(float x) {
+  const float s = 1.0f / (1.0f + expf(-x));
+  return s * (1.0f + x * (1.0f - s));
+}
+
+// ---------------------------------------------------------------------------
+// GroupNorm(1, C) backward, fused with what followed the normalisation in the forward
+// (kernels.h norm_kernel):  y = GN(r);  out = act ? GELU(y) : res ? GELU(res + y) : y;  out += emb.
+// Pass A (one block per sample): recompute the sample statistics from the conv epilogue's
+// partials (same order as the forward), dy = dout * GELU'(pre), and reduce the sample sums
+// S1 = sum(gamma dy), S2 = sum(gamma dy xhat) plus per-(sample, channel) partials of
+// dgamma = sum(dy xhat), dbeta = sum(dy), demb = sum(dout).  Pass B (grid (chunks, N)):
+// dr = rstd (gamma dy - S1/cnt - xhat S2/cnt); dres += dy (residual blocks).
+// ---------------------------------------------------------------------------
+struct GnBwdParams {
+  const float* r;        // raw conv output [N][HW][C]
+  const float2* rowpart; int nseg; int rrows;  // forward GroupNorm partials (stats recomputed)
+  const float* gamma; const float* beta;
+  const float* res;      // residual input of a residual ResBlock (or null)
+  int act;               // 1: out = GELU(y)
+  const float* dout;     // [N][HW][C]
+  int C, HW;
+  float* dr;             // [N][HW][C]
+  float* dres;           // residual gradient dy (res != null): dres_mode 1 writes, 2 accumulates
+  int dres_mode;
+  float* sums;           // [N][2]: S1, S2 (pass A out)
+  float* chpart;         // [N][2][C]: per-sample dgamma, dbeta partials (pass A out)
+  float* demb; int demb_stride, demb_off;  // or null: demb[n][off + c] = sum over pixels of dout
+};
+
+DMX_DEV float2 gn_stats_from_rowpart(const GnBwdParams& p, int n, double* red) {
+  // identical reduction to norm_kernel's (kernels.h): per-thread double sums, wave shuffles, 4 waves
+  const int tid = threadIdx.x;
+  const int cnt = p.rrows * p.nseg;
+  const float2* rp = p.rowpart + (size_t)n * cnt;
+  double s1 = 0.0, s2 = 0.0;
+  for (int i = tid; i < cnt; i += 256) {
+    const float2 q = rp[i];
+    s1 += (double)q.x;
+    s2 += (double)q.y;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
+  }
+  __syncthreads();
+  if ((tid & 63) == 0) {
+    red[tid >> 6] = s1;
+    red[4 + (tid >> 6)] = s2;
+  }
+  __syncthreads();
+  const double cntd = (double)p.HW * (double)p.C;
+  const double mean = ((red[0] + red[1]) + (red[2] + red[3])) / cntd;
+  double var = ((red[4] + red[5]) + (red[6] + red[7])) / cntd - mean * mean;
+  var = var < 0.0 ? 0.0 : var;
+  return make_float2((float)mean, (float)(1.0 / sqrt(var + 1e-5)));
+}
+
+DMX_DEV float gn_dy(const GnBwdParams& p, size_t idx, int c, float xh, float& dres_out) {
+  const float y = xh * p.gamma[c] + p.beta[c];
+  const float d = p.dout[idx];
+  dres_out = 0.f;
+  if (p.res != nullptr) {
+    const float dy = d * gelu_grad(p.res[idx] + y);
+    dres_out = dy;
+    return dy;
+  }
+  if (p.act) return d * gelu_grad(y);
+  return d;
+}
+
+// Thread -> (channels, pixels) ownership: C >= 256: channels tid + 256 q (q < C / 256), every
+// pixel; C < 256 (C | 256): channel tid % C, pixels tid / C + k (256 / C).  Coalesced rows.
+static __global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const GnBwdParams p) {
+  __shared__ double red[8];
+  __shared__ float tg[3][2][256];
+  __shared__ double sr[8];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  const float2 st = gn_stats_from_rowpart(p, n, red);
+  const bool wide = p.C >= 256;
+  const int cpt = wide ? p.C / 256 : 1, pstep = wide ? 1 : 256 / p.C;
+  const int c0 = wide ? tid : tid % p.C, p0 = wide ? 0 : tid / p.C;
+  const size_t base = (size_t)n * p.HW * p.C;
+  float s1 = 0.f, s2 = 0.f;
+  float g1[2] = {0.f, 0.f}, b1[2] = {0.f, 0.f}, e1[2] = {0.f, 0.f};
+  for (int pix = p0; pix < p.HW; pix += pstep) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      if (q >= cpt) break;
+      const int c = c0 + 256 * q;
+      const size_t idx = base + (size_t)pix * p.C + c;
+      const float xh = (p.r[idx] - st.x) * st.y;
+      float dres;
+      const float dy = gn_dy(p, idx, c, xh, dres);
+      const float gd = p.gamma[c] * dy;
+      s1 += gd;
+      s2 += gd * xh;
+      g1[q] += dy * xh;
+      b1[q] += dy;
+      e1[q] += p.dout[idx];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    tg[0][q][tid] = g1[q];
+    tg[1][q][tid] = b1[q];
+    tg[2][q][tid] = e1[q];
+  }
+  double d1 = s1, d2 = s2;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    d1 += __shfl_xor(d1, o, 64);
+    d2 += __shfl_xor(d2, o, 64);
+  }
+  if ((tid & 63) == 0) {
+    sr[tid >> 6] = d1;
+    sr[4 + (tid >> 6)] = d2;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    p.sums[2 * n] = (float)((sr[0] + sr[1]) + (sr[2] + sr[3]));
+    p.sums[2 * n + 1] = (float)((sr[4] + sr[5]) + (sr[6] + sr[7]));
+  }
+  // per-channel sums over the threads sharing a channel, in thread order (deterministic)
+  for (int c = tid; c < p.C; c += 256) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    if (wide) {
+      const int q = c / 256, t = c % 256;
+      a0 = tg[0][q][t];
+      a1 = tg[1][q][t];
+      a2 = tg[2][q][t];
+    } else {
+      for (int t = c; t < 256; t += p.C) {
+        a0 += tg[0][0][t];
+        a1 += tg[1][0][t];
+        a2 += tg[2][0][t];
+      }
+    }
+    p.chpart[((size_t)n * 2 + 0) * p.C + c] = a0;
+    p.chpart[((size_t)n * 2 + 1) * p.C + c] = a1;
+    if (p.demb != nullptr) p.demb[(size_t)n * p.demb_stride + p.demb_off + c] = a2;
+  }
+}
+
+static __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const GnBwdParams p) {
+  __shared__ double red[8];
+  const int n = blockIdx.y, tid = threadIdx.x;
+  const float2 st = gn_stats_from_rowpart(p, n, red);
+  const float cnt = (float)p.HW * (float)p.C;
+  const float m1 = p.sums[2 * n] / cnt, m2 = p.sums[2 * n + 1] / cnt;
+  const size_t base = (size_t)n * p.HW * p.C;
+  const int per = p.HW * p.C;
+  for (int i = blockIdx.x * 256 + tid; i < per; i += gridDim.x * 256) {
+    const int c = i % p.C;
+    const size_t idx = base + i;
+    const float xh = (p.r[idx] - st.x) * st.y;
+    float dres;
+    const float dy = gn_dy(p, idx, c, xh, dres);
+    p.dr[idx] = st.y * (p.gamma[c] * dy - m1 - xh * m2);
+    if (p.dres_mode == 1) p.dres[idx] = dres;
+    else if (p.dres_mode == 2) p.dres[idx] += dres;
+  }
+}
+
+// Column sums of [R][C] partial rows in row order (fixed): out[c] (+)= sum_r in[r * stride + c].
+static __global__ void colsum_kernel(const float* in, int R, int C, size_t stride, float* out, int accumulate) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int r = 0; r < R; ++r) s += in[(size_t)r * stride + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+
+// ---------------------------------------------------------------------------
+// LayerNorm backward (nn.LayerNorm over C, eps 1e-5; kernels.h layernorm_kernel): one wave per
+// token.  dx (+)= rstd (gamma dy - mean(gamma dy) - xhat mean(gamma dy xhat)); per-block
+// partials of dgamma / dbeta ([blocks][2][C], summed later by colsum_kernel).
+// ---------------------------------------------------------------------------
+template <int CPL>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const float* x, const float* w, const float* dy, float* dx,
+                                                     int accumulate, float* part, int M) {
+  constexpr int C = CPL * 64;
+  __shared__ float pg[4][C], pb[4][C];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + wv;
+  float v[CPL], g[CPL];
+  const bool ok = row < M;
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    v[j] = ok ? x[(size_t)row * C + lane + 64 * j] : 0.f;
+    s += v[j];
+  }
+  const float mean = wave_sum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const float d = v[j] - mean;
+    q += d * d;
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)C + 1e-5f);
+  float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    const int c = lane + 64 * j;
+    const float xh = (v[j] - mean) * rstd;
+    g[j] = ok ? dy[(size_t)row * C + c] : 0.f;
+    const float gd = g[j] * w[c];
+    a1 += gd;
+    a2 += gd * xh;
+    pg[wv][c] = g[j] * xh;
+    pb[wv][c] = g[j];
+  }
+  const float m1 = wave_sum(a1) / (float)C, m2 = wave_sum(a2) / (float)C;
+  if (ok) {
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const int c = lane + 64 * j;
+      const float xh = (v[j] - mean) * rstd;
+      const float r = rstd * (g[j] * w[c] - m1 - xh * m2);
+      float* o = dx + (size_t)row * C + c;
+      *o = accumulate ? *o + r : r;
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    part[((size_t)blockIdx.x * 2 + 0) * C + c] = (pg[0][c] + pg[1][c]) + (pg[2][c] + pg[3][c]);
+    part[((size_t)blockIdx.x * 2 + 1) * C + c] = (pb[0][c] + pb[1][c]) + (pb[2][c] + pb[3][c]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Weight gradient of an implicit GEMM (conv3x3 pad 1 or Linear):
+//   dW[co][k] = sum_m dY[m][co] * A[m][k],  A[m][k] = X at row m's tap (k = tap * Cin + ci)
+// on fp32 MFMA (v_mfma_f32_32x32x2_f32): block tile 64 (co) x 64 (k), 4 waves 2 x 2, the rows m
+// split into `splits` slabs (blockIdx.z) written to part[split][Cout][K]; wgrad_finish_kernel
+// sums the slabs in split order and scatters to the torch layout [Cout][Cin][3][3] / [Cout][Cin].
+// ---------------------------------------------------------------------------
+struct WgradParams {
+  const float* dy;   // [M][Cout]
+  const float* x;    // [N][H][W][Cin] (NHWC)
+  int N, H, W, Cin, Cout, taps;  // taps 9 (conv3x3) or 1 (linear)
+  int M, K;          // M = N*H*W rows, K = taps * Cin
+  int rows_per_split;
+  float* part;       // [splits][Cout][K]
+};
+
+static __global__ __launch_bounds__(256) void wgrad_kernel(const WgradParams p) {
+  constexpr int MK = 16;  // rows per LDS tile
+  __shared__ float dys[MK][64 + 4];
+  __shared__ float xs[MK][64 + 4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv >> 1, wn = wv & 1;
+  const int co0 = blockIdx.x * 64, k0 = blockIdx.y * 64;
+  const int mbeg = blockIdx.z * p.rows_per_split, mend = min(p.M, mbeg + p.rows_per_split);
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  const int HW = p.H * p.W;
+  for (int m0 = mbeg; m0 < mend; m0 += MK) {
+    // stage 16 rows x 64 co of dY and 16 rows x 64 k of the tapped input
+    for (int i = tid; i < MK * 64; i += 256) {
+      const int r = i >> 6, c = i & 63, m = m0 + r;
+      const int co = co0 + c, k = k0 + c;
+      dys[r][c] = (m < mend && co < p.Cout) ? p.dy[(size_t)m * p.Cout + co] : 0.f;
+      float xv = 0.f;
+      if (m < mend && k < p.K) {
+        const int tap = k / p.Cin, ci = k - tap * p.Cin;
+        const int n = m / HW, rr = m - n * HW, y = rr / p.W, xx = rr - y * p.W;
+        int iy = y, ix = xx;
+        if (p.taps == 9) {
+          iy = y + tap / 3 - 1;
+          ix = xx + tap % 3 - 1;
+        }
+        if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W) xv = p.x[(((size_t)n * p.H + iy) * p.W + ix) * p.Cin + ci];
+      }
+      xs[r][c] = xv;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < MK; s += 2) {
+      const float a = dys[s + (lane >> 5)][wm * 32 + (lane & 31)];
+      const float b = xs[s + (lane >> 5)][wn * 32 + (lane & 31)];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  float* dst = p.part + (size_t)blockIdx.z * p.Cout * p.K;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int co = co0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    const int k = k0 + wn * 32 + (lane & 31);
+    if (co < p.Cout && k < p.K) dst[(size_t)co * p.K + k] = acc[r];
+  }
+}
+
+// grad (torch layout) = sum over splits (split order); k = tap * Cin + ci -> [co][ci][tap]
+// (input channels >= cin_real — the zero padding of a 3-channel input — are dropped).
+static __global__ void wgrad_finish_kernel(const float* part, int splits, int Cout, int Cin, int cin_real, int taps,
+                                           float* grad) {
+  const int K = taps * Cin;
+  const size_t total = (size_t)Cout * K;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const int co = (int)(i / K), k = (int)(i % K), tap = k / Cin, ci = k - tap * Cin;
+    if (ci >= cin_real) continue;
+    float s = 0.f;
+    for (int z = 0; z < splits; ++z) s += part[(size_t)z * total + i];
+    grad[((size_t)co * cin_real + ci) * taps + tap] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Elementwise / layout helpers.
+// ---------------------------------------------------------------------------
+// dst (+)= src * GELU'(pre)
+static __global__ void gelu_bwd_kernel(const float* d, const float* pre, float* dst, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    dst[i] = d[i] * gelu_grad(pre[i]);
+}
+static __global__ void gelu_fwd_kernel(const float* x, float* y, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) y[i] = gelu(x[i]);
+}
+static __global__ void add_kernel(float* dst, const float* src, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) dst[i] += src[i];
+}
+
+// max_pool2d(2) backward (floor mode): the gradient goes to the first maximum of each window in
+// (0,0), (0,1), (1,0), (1,1) order (strict >, torch's CPU kernel); uncovered rows / columns get 0.
+// x: [N][Hs][Ws][C], dy: [N][Hs/2][Ws/2][C]; dx (+)= (accumulate).
+static __global__ void maxpool_bwd_kernel(const float* src, const float* dy, float* dx, int N, int Hs, int Ws, int C,
+                                          int accumulate) {
+  const int Ho = Hs / 2, Wo = Ws / 2;
+  const size_t total = (size_t)N * Hs * Ws * C;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const int c = (int)(i % C);
+    const size_t pix = i / C;
+    const int n = (int)(pix / ((size_t)Hs * Ws)), rr = (int)(pix % ((size_t)Hs * Ws)), y = rr / Ws, x = rr % Ws;
+    const int oy = y >> 1, ox = x >> 1;
+    float g = 0.f;
+    if (oy < Ho && ox < Wo) {
+      const float* b = src + (((size_t)n * Hs + 2 * oy) * Ws + 2 * ox) * C + c;
+      const float v[4] = {b[0], b[C], b[(size_t)Ws * C], b[(size_t)Ws * C + C]};
+      int am = 0;
+      for (int k = 1; k < 4; ++k)
+        if (v[k] > v[am]) am = k;
+      if (am == (y & 1) * 2 + (x & 1)) g = dy[(((size_t)n * Ho + oy) * Wo + ox) * C + c];
+    }
+    dx[i] = accumulate ? dx[i] + g : g;
+  }
+}
+
+// Up's input backward: dcat [N][H][W][C0 + C1] -> dskip (+)= dcat[..., :C0] and the low-resolution
+// map's gradient (+)= bilinear-x2 (align_corners) adjoint of the un-padded dcat[..., C0:].  Gather
+// form: each low-res pixel (i, j) sums w_y(oy, i) w_x(ox, j) d(oy, ox) over the output pixels whose
+// interpolation touches it (same weights as source.h upsample4).
+static __global__ void upcat_bwd_kernel(const float* dcat, float* dskip, float* dlow, int N, int H, int W, int C0,
+                                        int C1, int Hs, int Ws, int padT, int padL, int acc_skip, int acc_low) {
+  const int C = C0 + C1;
+  const size_t tot_skip = (size_t)N * H * W * C0;
+  const size_t tot_low = (size_t)N * Hs * Ws * C1;
+  const size_t stride = (size_t)gridDim.x * 256;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < tot_skip + tot_low; i += stride) {
+    if (i < tot_skip) {
+      const int c = (int)(i % C0);
+      const size_t pix = i / C0;
+      const float g = dcat[pix * C + c];
+      dskip[i] = acc_skip ? dskip[i] + g : g;
+      continue;
+    }
+    const size_t j = i - tot_skip;
+    const int c = (int)(j % C1);
+    const size_t pix = j / C1;
+    const int n = (int)(pix / ((size_t)Hs * Ws)), rr = (int)(pix % ((size_t)Hs * Ws)), li = rr / Ws, lj = rr % Ws;
+    const int Ho = 2 * Hs, Wo = 2 * Ws;
+    const float sh = Ho > 1 ? (float)(Hs - 1) / (float)(Ho - 1) : 0.f;
+    const float sw = Wo > 1 ? (float)(Ws - 1) / (float)(Wo - 1) : 0.f;
+    float g = 0.f;
+    // output rows / columns whose interpolation can touch (li, lj): floor(sh * u) in {li - 1, li}
+    const int uy0 = sh > 0.f ? max(0, (int)floorf((float)(li - 1) / sh) - 1) : 0;
+    const int uy1 = sh > 0.f ? min(Ho - 1, (int)ceilf((float)(li + 1) / sh) + 1) : Ho - 1;
+    const int ux0 = sw > 0.f ? max(0, (int)floorf((float)(lj - 1) / sw) - 1) : 0;
+    const int ux1 = sw > 0.f ? min(Wo - 1, (int)ceilf((float)(lj + 1) / sw) + 1) : Wo - 1;
+    for (int uy = uy0; uy <= uy1; ++uy) {
+      const float fy = sh * (float)uy;
+      const int y0 = (int)fy, y1 = y0 + (y0 < Hs - 1 ? 1 : 0);
+      const float ly = fminf(fmaxf(fy - (float)y0, 0.f), 1.f), hy = 1.f - ly;
+      float wy = 0.f;
+      if (y0 == li) wy += hy;
+      if (y1 == li) wy += ly;
+      if (wy == 0.f) continue;
+      const int oy = uy + padT;
+      if (oy < 0 || oy >= H) continue;
+      for (int ux = ux0; ux <= ux1; ++ux) {
+        const float fx = sw * (float)ux;
+        const int x0 = (int)fx, x1 = x0 + (x0 < Ws - 1 ? 1 : 0);
+        const float lx = fminf(fmaxf(fx - (float)x0, 0.f), 1.f), hx = 1.f - lx;
+        float wx = 0.f;
+        if (x0 == lj) wx += hx;
+        if (x1 == lj) wx += lx;
+        if (wx == 0.f) continue;
+        const int ox = ux + padL;
+        if (ox < 0 || ox >= W) continue;
+        g += wy * wx * dcat[(((size_t)n * H + oy) * W + ox) * C + C0 + c];
+      }
+    }
+    dlow[j] = acc_low ? dlow[j] + g : g;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Multi-head attention core backward (fp32), per (sample, head):
+//   P = softmax(Q K^T / sqrt D), O = P V;  given dO:
+//   Dlt_i = sum_d dO_i O_i;  dS = P (dO V^T - Dlt);  dQ = dS K / sqrt D;  dK = dS^T Q / sqrt D;  dV = P^T dO.
+// attn_rowstats_kernel: per query row max m_i, sum l_i of exp(s - m) and Dlt_i (one thread per row).
+// attn_dq_kernel: one thread per query row, keys streamed through LDS in 64-key tiles.
+// attn_dkv_kernel: one thread per key, queries streamed through LDS.
+// qkv: [N][L][3C] (q | k | v, head h at columns h*D), o / dO: [N][L][C]; dqkv: [N][L][3C].
+// ---------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(64) void attn_rowstats_kernel(const float* qkv, const float* o, const float* dout,
+                                                           float* st, int L, int C) {
+  __shared__ float ks[64][D];
+  const int hd = blockIdx.y, n = blockIdx.z, i = blockIdx.x * 64 + threadIdx.x;
+  const size_t rs = 3 * (size_t)C;
+  const float* base = qkv + (size_t)n * L * rs;
+  const float sc = 1.0f / sqrtf((float)D);
+  float q[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) q[d] = i < L ? base[(size_t)i * rs + hd * D + d] * sc : 0.f;
+  float m = -INFINITY, l = 0.f;
+  for (int j0 = 0; j0 < L; j0 += 64) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < 64 * D; e += 64) {
+      const int j = e / D, d = e % D;
+      ks[j][d] = j0 + j < L ? base[(size_t)(j0 + j) * rs + C + hd * D + d] : 0.f;
+    }
+    __syncthreads();
+    for (int j = 0; j < 64 && j0 + j < L; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) s += q[d] * ks[j][d];
+      if (s > m) {
+        l = l * expf(m - s) + 1.f;
+        m = s;
+      } else {
+        l += expf(s - m);
+      }
+    }
+  }
+  if (i < L) {
+    float dl = 0.f;
+    const size_t ob = ((size_t)n * L + i) * C + hd * D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) dl += dout[ob + d] * o[ob + d];
+    float* s = st + (((size_t)n * 4 + hd) * L + i) * 3;
+    s[0] = m;
+    s[1] = l;
+    s[2] = dl;
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(64) void attn_dq_kernel(const float* qkv, const float* dout, const float* st, float* dqkv,
+                                                     int L, int C) {
+  __shared__ float ks[64][D], vs[64][D];
+  const int hd = blockIdx.y, n = blockIdx.z, i = blockIdx.x * 64 + threadIdx.x;
+  const size_t rs = 3 * (size_t)C;
+  const float* base = qkv + (size_t)n * L * rs;
+  const float sc = 1.0f / sqrtf((float)D);
+  float q[D], g[D], dq[D];
+  const size_t ob = ((size_t)n * L + min(i, L - 1)) * C + hd * D;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    q[d] = i < L ? base[(size_t)i * rs + hd * D + d] * sc : 0.f;
+    g[d] = i < L ? dout[ob + d] : 0.f;
+    dq[d] = 0.f;
+  }
+  const float* s3 = st + (((size_t)n * 4 + hd) * L + min(i, L - 1)) * 3;
+  const float m = s3[0], il = 1.0f / s3[1], dl = s3[2];
+  for (int j0 = 0; j0 < L; j0 += 64) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < 64 * D; e += 64) {
+      const int j = e / D, d = e % D;
+      const bool ok = j0 + j < L;
+      ks[j][d] = ok ? base[(size_t)(j0 + j) * rs + C + hd * D + d] : 0.f;
+      vs[j][d] = ok ? base[(size_t)(j0 + j) * rs + 2 * C + hd * D + d] : 0.f;
+    }
+    __syncthreads();
+    for (int j = 0; j < 64 && j0 + j < L; ++j) {
+      float s = 0.f, dp = 0.f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        s += q[d] * ks[j][d];
+        dp += g[d] * vs[j][d];
+      }
+      const float ds = expf(s - m) * il * (dp - dl);
+#pragma unroll
+      for (int d = 0; d < D; ++d) dq[d] += ds * ks[j][d];
+    }
+  }
+  if (i < L) {
+    float* dst = dqkv + ((size_t)n * L + i) * rs + hd * D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) dst[d] = dq[d] * sc;
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(64) void attn_dkv_kernel(const float* qkv, const float* dout, const float* st, float* dqkv,
+                                                      int L, int C) {
+  __shared__ float qs[64][D], gs[64][D], ss[64][3];
+  const int hd = blockIdx.y, n = blockIdx.z, j = blockIdx.x * 64 + threadIdx.x;
+  const size_t rs = 3 * (size_t)C;
+  const float* base = qkv + (size_t)n * L * rs;
+  const float sc = 1.0f / sqrtf((float)D);
+  float k[D], v[D], dk[D], dv[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    k[d] = j < L ? base[(size_t)j * rs + C + hd * D + d] : 0.f;
+    v[d] = j < L ? base[(size_t)j * rs + 2 * C + hd * D + d] : 0.f;
+    dk[d] = dv[d] = 0.f;
+  }
+  for (int i0 = 0; i0 < L; i0 += 64) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < 64 * D; e += 64) {
+      const int i = e / D, d = e % D;
+      const bool ok = i0 + i < L;
+      qs[i][d] = ok ? base[(size_t)(i0 + i) * rs + hd * D + d] * sc : 0.f;
+      gs[i][d] = ok ? dout[((size_t)n * L + i0 + i) * C + hd * D + d] : 0.f;
+    }
+    if (i0 + (int)threadIdx.x < L) {
+      const float* s3 = st + (((size_t)n * 4 + hd) * L + i0 + threadIdx.x) * 3;
+      ss[threadIdx.x][0] = s3[0];
+      ss[threadIdx.x][1] = 1.0f / s3[1];
+      ss[threadIdx.x][2] = s3[2];
+    }
+    __syncthreads();
+    for (int i = 0; i < 64 && i0 + i < L; ++i) {
+      float s = 0.f, dp = 0.f;
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        s += qs[i][d] * k[d];
+        dp += gs[i][d] * v[d];
+      }
+      const float pr = expf(s - ss[i][0]) * ss[i][1];
+      const float ds = pr * (dp - ss[i][2]);
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        dv[d] += pr * gs[i][d];
+        dk[d] += ds * qs[i][d];  // qs already carries the 1/sqrt(D)
+      }
+    }
+  }
+  if (j < L) {
+    float* dst = dqkv + ((size_t)n * L + j) * rs + hd * D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      dst[C + d] = dk[d];
+      dst[2 * C + d] = dv[d];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Small dense layers (embedding MLPs, emb heads, GeomHead), R <= a few hundred rows:
+//   forward y = x W^T + b over [R][K] -> [R][O]; backward dW = dY^T X, db = sum_r dY, dX = dY W.
+// One thread per output element, rows / inputs summed in order (deterministic).
+// ---------------------------------------------------------------------------
+static __global__ void dense_dw_kernel(const float* dy, int ldy, const float* x, int ldx, int R, int O, int K,
+                                       float* dw, float* db) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < (size_t)O * K) {
+    const int o = (int)(i / K), k = (int)(i % K);
+    float s = 0.f;
+    for (int r = 0; r < R; ++r) s += dy[(size_t)r * ldy + o] * x[(size_t)r * ldx + k];
+    dw[i] = s;
+  } else if (db != nullptr && i < (size_t)O * K + O) {
+    const int o = (int)(i - (size_t)O * K);
+    float s = 0.f;
+    for (int r = 0; r < R; ++r) s += dy[(size_t)r * ldy + o];
+    db[o] = s;
+  }
+}
+// dX[r][k] (+)= sum_o dY[r][o] W[o][k]  (W row-major [O][K])
+static __global__ void dense_dx_kernel(const float* dy, int ldy, const float* w, int R, int O, int K, float* dx, int ldx,
+                                       int accumulate) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)R * K) return;
+  const int r = (int)(i / K), k = (int)(i % K);
+  float s = 0.f;
+  for (int o = 0; o < O; ++o) s += dy[(size_t)r * ldy + o] * w[(size_t)o * K + k];
+  float* d = dx + (size_t)r * ldx + k;
+  *d = accumulate ? *d + s : s;
+}
+// y = x W^T + b (forward for the small layers of the training tape)
+static __global__ void dense_fwd_kernel(const float* x, int ldx, const float* w, const float* b, int R, int O, int K,
+                                        float* y, int ldy) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)R * O) return;
+  const int r = (int)(i / O), o = (int)(i % O);
+  float s = b != nullptr ? b[o] : 0.f;
+  for (int k = 0; k < K; ++k) s += x[(size_t)r * ldx + k] * w[(size_t)o * K + k];
+  y[(size_t)r * ldy + o] = s;
+}
+static __global__ void silu_fwd_kernel(const float* x, float* y, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) y[i] = silu(x[i]);
+}
+static __global__ void silu_bwd_kernel(const float* d, const float* pre, float* dst, size_t n, int accumulate) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    const float g = d[i] * silu_grad(pre[i]);
+    dst[i] = accumulate ? dst[i] + g : g;
+  }
+}
+
+// Layout helpers: NCHW <-> NHWC (channels padded to Cp with zeros), [vals | mask] concat.
+static __global__ void nchw_to_nhwc_kernel(const float* src, float* dst, int N, int C, int Cp, int HW) {
+  const size_t total = (size_t)N * HW * Cp;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const int c = (int)(i % Cp);
+    const size_t pix = i / Cp;
+    const int n = (int)(pix / HW), hw = (int)(pix % HW);
+    dst[i] = c < C ? src[((size_t)n * C + c) * HW + hw] : 0.f;
+  }
+}
+static __global__ void cat24_kernel(const float* vals, const float* mask, float* out, int N) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= N * 24) return;
+  const int n = i / 24, k = i % 24;
+  out[i] = k < 12 ? vals[n * 12 + k] : mask[n * 12 + k - 12];
+}
+
+// GAP (mean over HW) of feat [N][HW][64] -> g [N][64]; and its backward dfeat[n][hw][k] += dg[n][k] / HW.
+static __global__ void gap_fwd_kernel(const float* feat, int HW, float* g) {
+  const int n = blockIdx.x, k = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  __shared__ float part[4][64];
+  float s = 0.f;
+  for (int pix = sl; pix < HW; pix += 4) s += feat[((size_t)n * HW + pix) * 64 + k];
+  part[sl][k] = s;
+  __syncthreads();
+  if (threadIdx.x < 64) g[n * 64 + threadIdx.x] = (part[0][threadIdx.x] + part[1][threadIdx.x] +
+                                                   part[2][threadIdx.x] + part[3][threadIdx.x]) / (float)HW;
+}
+static __global__ void gap_bwd_kernel(const float* dg, int N, int HW, float* dfeat) {
+  const size_t total = (size_t)N * HW * 64;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const int k = (int)(i % 64), n = (int)(i / ((size_t)HW * 64));
+    dfeat[i] += dg[n * 64 + k] / (float)HW;
+  }
+}
+
+// Per-channel sum of dY [M][C] (bias gradients of Linear layers / conv biases): part[blocks][C].
+static __global__ __launch_bounds__(256) void rowsum_part_kernel(const float* dy, int M, int C, int rows_per_block,
+                                                                 float* part) {
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f;
+    for (int r = r0; r < r1; ++r) s += dy[(size_t)r * C + c];
+    part[(size_t)blockIdx.x * C + c] = s;
+  }
+}
+
+// Embedding (models/unet_cond.py:155-167): emb[n] = pos(t_n) + class_emb[y_n] (+ cond, added by the
+// host sequence); dclass[c][k] = sum over samples with y_n == c of demb[n][k] (sample order).
+static __global__ void embed_base_kernel(const int64_t* t, const int64_t* y, const float* pos_table, int tmax,
+                                         const float* class_emb, int ncls, float* emb) {
+  const int n = blockIdx.x, k = threadIdx.x;
+  int64_t tt = t[n];
+  tt = tt < 1 ? 1 : (tt > tmax ? tmax : tt);
+  float v = pos_table[(size_t)(tt - 1) * 256 + k];
+  if (y != nullptr) {
+    int64_t yy = y[n];
+    yy = yy < 0 ? 0 : (yy >= ncls ? ncls - 1 : yy);
+    v += class_emb[yy * 256 + k];
+  }
+  emb[n * 256 + k] = v;
+}
+static __global__ void class_emb_bwd_kernel(const float* demb, const int64_t* y, int N, int ncls, float* dclass) {
+  const int c = blockIdx.x, k = threadIdx.x;
+  float s = 0.f;
+  for (int n = 0; n < N; ++n)
+    if (y[n] == c) s += demb[n * 256 + k];
+  dclass[c * 256 + k] = s;
+}
+
+}  // namespace dmx

@@ -1,0 +1,779 @@
+// dmx — training step of the conditional U-Net: the forward with a tape
+// and the backward pass of UnetCond / UnetCondWithGeomHead, as train_latent_cond.py:136-163
+// runs them (model(z_noisy, t, y, cond_vals, cond_mask) -> F.mse_loss + masked_geom_mse ->
+// loss.backward(); the loss itself and Adam stay in torch).
+//
+// Forward = the inference trunk's kernels in exact-fp32 mode (fp32 MFMA implicit GEMMs, no
+// deferred split-K fusion so every raw conv output is materialised) plus the few values the
+// backward needs that inference never stores (pre-GELU FF activations, embedding MLP inputs).
+// The tape lives in its own workspace (m->tws) until the matching dmx_train_backward.
+// Backward (train.h kernels + the same fp32 implicit GEMM for data gradients):
+//   GroupNorm / LayerNorm / GELU / SiLU / max-pool / bilinear-upsample adjoints, conv and Linear
+//   data gradients as implicit GEMMs over flipped / transposed weights (packed once, refreshed
+//   with the weights), weight gradients on fp32 MFMA (wgrad_kernel), attention core backward by
+//   recomputation.  Parameter gradients are written in the reference's state_dict layout.
+//
+// Included by engine.hip after the inference engine (same translation unit).
+#pragma once
+
+namespace dmx {
+
+struct TRes {  // one ResBlock of the training forward (models/unet_cond.py:10-30)
+  const ResW* w = nullptr;
+  int N = 0, H = 0, W = 0;
+  bool residual = false;
+  const float* x = nullptr;  // NHWC input (also the residual)
+  float *r1 = nullptr, *a1 = nullptr, *r2 = nullptr, *out = nullptr;
+  float2 *rp1 = nullptr, *rp2 = nullptr;
+  int rr1 = 0, rr2 = 0;
+  int emb_off = -1;  // >= 0: out += emb head slice (Down / Up, unet_cond.py:69,99)
+};
+struct TAttn {  // one AttenionBlock (models/unet_cond.py:32-52)
+  const AttnW* w = nullptr;
+  int N = 0, H = 0, W = 0;
+  const float* x = nullptr;
+  float *xl = nullptr, *qkv = nullptr, *ao = nullptr, *av = nullptr, *al = nullptr, *h1 = nullptr, *f = nullptr,
+        *out = nullptr;
+};
+struct TUp {  // Up's bilinear x2 + pad + concat input (models/unet_cond.py:87-97)
+  float* cat = nullptr;
+  const float* skip = nullptr;
+  const float* low = nullptr;
+  int C0 = 0, C1 = 0, H = 0, W = 0, Hs = 0, Ws = 0, padT = 0, padL = 0;
+};
+
+struct Tape {
+  int64_t id = 0;
+  int n = 0, h = 0, w = 0;
+  bool cond = false;  // cond_vals / cond_mask given (unet_cond_geom.py:91)
+  int64_t* y = nullptr;
+  float *xin = nullptr, *in24 = nullptr, *v0 = nullptr, *ca = nullptr, *ch = nullptr, *v = nullptr, *s = nullptr,
+        *heads = nullptr;
+  TRes inc;
+  const float* skip[3] = {nullptr, nullptr, nullptr};
+  int sh[3] = {0, 0, 0}, sw[3] = {0, 0, 0}, sc[3] = {0, 0, 0};
+  float* pooled[3] = {nullptr, nullptr, nullptr};
+  TRes dr0[3], dr1[3], bot[3], ur0[3], ur1[3];
+  TAttn dsa[3], usa[3];
+  TUp up[3];
+  const float* feat = nullptr;
+  float *g = nullptr, *hpre = nullptr, *hs = nullptr;
+};
+
+static int ew_blocks(size_t n) { return (int)std::min<size_t>((n + 255) / 256, 8192); }
+
+static const float* srcp(dmx_model* m, const std::string& name) {
+  auto it = m->inputs.find(name);
+  if (it == m->inputs.end()) throw Error(DMX_E_STATE, "registered tensor '" + name + "' missing");
+  return it->second.first;
+}
+
+// Gradient destinations, one per state_dict key (dmx_model_cfg_key order).
+struct GradMap {
+  std::map<std::string, float*> g;
+  float* operator()(const std::string& name) const {
+    auto it = g.find(name);
+    if (it == g.end() || it->second == nullptr) throw Error(DMX_E_ARG, "no gradient buffer for '" + name + "'");
+    return it->second;
+  }
+};
+
+// Workspace run twice (plan: sizes only, then real) in a dedicated arena.
+template <typename F>
+static void run_arena(dmx_model* m, hipStream_t st, Arena& A, void*& mem, size_t& cap, F&& body) {
+  A.base = nullptr;
+  A.off = 0;
+  A.plan = true;
+  {
+    Run R{m, st, true, A};
+    body(R);
+  }
+  if (A.off > cap) {
+    if (mem) {
+      HIPCHK(hipStreamSynchronize(st));
+      HIPCHK(hipFree(mem));
+    }
+    mem = nullptr;
+    cap = 0;
+    HIPCHK(hipMalloc(&mem, A.off));
+    cap = A.off;
+  }
+  A.base = static_cast<char*>(mem);
+  A.off = 0;
+  A.plan = false;
+  Run R{m, st, false, A};
+  body(R);
+}
+
+// ---------------------------------------------------------------------------
+// data-gradient weights (packed once on the first training call, refreshed with the rest)
+// ---------------------------------------------------------------------------
+static __global__ void flip_transpose3x3_kernel(float* dst, const float* src, int cout, int cin) {
+  const size_t total = (size_t)cout * cin * 9;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
+    const int t = (int)(i % 9);
+    const size_t r = i / 9;
+    const int co = (int)(r % cout), ci = (int)(r / cout);  // dst [ci][co][t] = src [co][ci][8 - t]
+    dst[i] = src[((size_t)co * cin + ci) * 9 + (8 - t)];
+  }
+}
+
+// conv3x3 pad 1 [cout][cin] -> its data gradient: conv3x3 pad 1 over dY with the kernel flipped
+// and the channel roles swapped (cin' = cout, cout' = cin).
+static ConvW pack_dgrad_conv(Packer& P, const std::string& wname, int cin, int cout) {
+  ConvW c;
+  c.cin = cout;
+  c.cout = cin;
+  c.taps = 9;
+  c.kpad = rup(9 * cout, 64);
+  c.npad = rup(cin, 128);
+  c.B = P.alloc((size_t)c.npad * c.kpad);
+  float* tmp = P.alloc((size_t)cin * cout * 9);
+  const float* src = P.in(wname).first;
+  P.job([=](hipStream_t s) {
+    flip_transpose3x3_kernel<<<ew_blocks((size_t)cin * cout * 9), 256, 0, s>>>(tmp, src, cout, cin);
+    HIPCHK(hipGetLastError());
+  });
+  P.repack(c.B, tmp, 0, 1, c.npad, c.kpad, cin, cout, 3);
+  return c;
+}
+
+// Linear [fout][fin] -> dX = dY W: a Linear with weight W^T [fin][fout].
+static ConvW pack_dgrad_linear(Packer& P, const std::string& wname, int fin, int fout) {
+  ConvW c;
+  c.cin = fout;
+  c.cout = fin;
+  c.taps = 1;
+  c.kpad = rup(fout, 64);
+  c.npad = rup(fin, 128);
+  c.B = P.alloc((size_t)c.npad * c.kpad);
+  float* tmp = P.transposed(wname, fout, fin);
+  P.repack(c.B, tmp, 1, 1, c.npad, c.kpad, fin, fout, 1);
+  return c;
+}
+
+static void ensure_train(dmx_model* m, hipStream_t st) {
+  if (m->train_ready) return;
+  Packer P{m, st};
+  auto res = [&](ResW& r, bool need_dx) {
+    if (need_dx) r.d1 = pack_dgrad_conv(P, r.prefix + ".double_conv.0.weight", r.cin, r.mid);
+    r.d2 = pack_dgrad_conv(P, r.prefix + ".double_conv.3.weight", r.mid, r.cout);
+  };
+  res(m->inc, false);  // the network input takes no gradient
+  for (int i = 0; i < 3; ++i) {
+    res(m->down[i].r0, true);
+    res(m->down[i].r1, true);
+    res(m->up[i].r0, true);
+    res(m->up[i].r1, true);
+  }
+  for (int i = 0; i < m->nbot; ++i) res(m->bot[i], true);
+  for (auto& a : m->sa) {
+    const int c = a.c;
+    a.dqkv = pack_dgrad_linear(P, a.prefix + ".mha.in_proj_weight", c, 3 * c);
+    a.dout = pack_dgrad_linear(P, a.prefix + ".mha.out_proj.weight", c, c);
+    a.df1 = pack_dgrad_linear(P, a.prefix + ".ff_self.1.weight", c, c);
+    a.df2 = pack_dgrad_linear(P, a.prefix + ".ff_self.3.weight", c, c);
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  m->train_ready = true;
+}
+
+// ---------------------------------------------------------------------------
+// training forward
+// ---------------------------------------------------------------------------
+static void dense_fwd(Run& R, const float* x, int ldx, const float* w, const float* b, int rows, int O, int K, float* y,
+                      int ldy) {
+  if (R.plan) return;
+  dense_fwd_kernel<<<ew_blocks((size_t)rows * O), 256, 0, R.st>>>(x, ldx, w, b, rows, O, K, y, ldy);
+  HIPCHK(hipGetLastError());
+}
+
+static TRes train_res(Run& R, const ResW& w, const float* x, int N, int H, int W, bool residual, const float* emb,
+                      int emb_stride, int emb_off) {
+  TRes t;
+  t.w = &w;
+  t.N = N;
+  t.H = H;
+  t.W = W;
+  t.residual = residual;
+  t.x = x;
+  const int M = N * H * W, HW = H * W, seg = 32;
+  t.r1 = R.ws.get<float>((size_t)M * w.mid);
+  t.rp1 = R.ws.get<float2>((size_t)M * (w.mid / seg));
+  t.a1 = R.ws.get<float>((size_t)M * w.mid);
+  t.r2 = R.ws.get<float>((size_t)M * w.cout);
+  t.rp2 = R.ws.get<float2>((size_t)M * (w.cout / seg));
+  t.out = R.ws.get<float>((size_t)M * w.cout);
+  t.rr1 = gemm(R, plain_src(x, w.cin), SRC_PLAIN, N, H, W, w.c1, EPI_STATS, t.r1, nullptr, t.rp1, seg);
+  NormParams n1 = norm_params(t.r1, t.rp1, w.mid / seg, t.rr1, w.g1.p, w.b1.p, w.mid, HW, t.a1);
+  n1.act = 1;
+  norm(R, n1, N);
+  t.rr2 = gemm(R, plain_src(t.a1, w.mid), SRC_PLAIN, N, H, W, w.c2, EPI_STATS, t.r2, nullptr, t.rp2, seg);
+  NormParams n2 = norm_params(t.r2, t.rp2, w.cout / seg, t.rr2, w.g2.p, w.b2.p, w.cout, HW, t.out);
+  if (residual) n2.res = x;
+  if (emb != nullptr) {
+    n2.emb = emb;
+    n2.emb_stride = emb_stride;
+    n2.emb_off = emb_off;
+    t.emb_off = emb_off;
+  }
+  norm(R, n2, N);
+  return t;
+}
+
+static TAttn train_attn(Run& R, const AttnW& a, const float* x, int N, int H, int W) {
+  TAttn t;
+  t.w = &a;
+  t.N = N;
+  t.H = H;
+  t.W = W;
+  t.x = x;
+  const int C = a.c, M = N * H * W, L = H * W;
+  t.xl = R.ws.get<float>((size_t)M * C);
+  t.qkv = R.ws.get<float>((size_t)M * 3 * C);
+  t.ao = R.ws.get<float>((size_t)M * C);
+  t.av = R.ws.get<float>((size_t)M * C);
+  t.al = R.ws.get<float>((size_t)M * C);
+  t.h1 = R.ws.get<float>((size_t)M * C);
+  t.f = R.ws.get<float>((size_t)M * C);
+  t.out = R.ws.get<float>((size_t)M * C);
+  layernorm(R, x, t.xl, a.l1w, a.l1b, M, C);
+  gemm(R, plain_src(t.xl, C), SRC_PLAIN, N, H, W, a.qkv, EPI_BIAS, t.qkv, nullptr, nullptr, 1);
+  attention_core(R, t.qkv, t.ao, N, L, C);
+  gemm(R, plain_src(t.ao, C), SRC_PLAIN, N, H, W, a.o, EPI_BIAS_RES, t.av, t.xl, nullptr, 1);
+  layernorm(R, t.av, t.al, a.l2w, a.l2b, M, C);
+  gemm(R, plain_src(t.al, C), SRC_PLAIN, N, H, W, a.f1, EPI_BIAS, t.h1, nullptr, nullptr, 1);
+  if (!R.plan) {
+    gelu_fwd_kernel<<<ew_blocks((size_t)M * C), 256, 0, R.st>>>(t.h1, t.f, (size_t)M * C);
+    HIPCHK(hipGetLastError());
+  }
+  gemm(R, plain_src(t.f, C), SRC_PLAIN, N, H, W, a.f2, EPI_BIAS_RES, t.out, t.av, nullptr, 1);
+  return t;
+}
+
+struct TrainArgs {
+  const float* x;  // NCHW
+  const int64_t* t;
+  const int64_t* y;
+  const float* vals;
+  const float* mask;
+  int n, h, w;
+  float* eps;   // NCHW out
+  float* geom;  // [n][geom_dim] out (UnetCondWithGeomHead) or null
+};
+
+static const char* kEmbHeads[6] = {"down1", "down2", "down3", "up1", "up2", "up3"};
+
+static void emb_head_slices(dmx_model* m, int off[6], int hc[6]) {
+  for (int i = 0; i < 3; ++i) {
+    off[i] = m->down[i].emb_off;
+    hc[i] = m->down[i].cout;
+    off[3 + i] = m->up[i].emb_off;
+    hc[3 + i] = m->up[i].cout;
+  }
+}
+
+static void train_fwd_body(Run& R, Tape& T, const TrainArgs& a) {
+  dmx_model* m = R.m;
+  const int N = a.n, H = a.h, W = a.w, HW = H * W;
+  T.n = N;
+  T.h = H;
+  T.w = W;
+  T.cond = a.vals != nullptr;
+  T.xin = R.ws.get<float>((size_t)N * HW * m->inc.cin);
+  T.y = R.ws.get<int64_t>(N);
+  T.v0 = R.ws.get<float>((size_t)N * 256);
+  T.v = R.ws.get<float>((size_t)N * 256);
+  T.s = R.ws.get<float>((size_t)N * 256);
+  T.heads = R.ws.get<float>((size_t)N * m->hsum);
+  if (T.cond) {
+    T.in24 = R.ws.get<float>((size_t)N * 24);
+    T.ca = R.ws.get<float>((size_t)N * 256);
+    T.ch = R.ws.get<float>((size_t)N * 256);
+  }
+  // embedding: emb = pos(t) + class_emb(y) (+ cond_mlp([vals, mask])), heads SiLU -> Linear
+  // (models/unet_cond.py:155-167, unet_cond_geom.py:89-95, unet_cond.py:62-65 / 82-85)
+  if (!R.plan) {
+    R.layer = "train.embed";
+    nchw_to_nhwc_kernel<<<ew_blocks((size_t)N * HW * m->inc.cin), 256, 0, R.st>>>(a.x, T.xin, N, m->in_ch,
+                                                                                 m->inc.cin, HW);
+    HIPCHK(hipMemcpyAsync(T.y, a.y, (size_t)N * sizeof(int64_t), hipMemcpyDeviceToDevice, R.st));
+    embed_base_kernel<<<N, 256, 0, R.st>>>(a.t, T.y, m->ctx->pos_table, m->ctx->tmax, srcp(m, "class_emb.weight"),
+                                           m->cfg.ncls, T.v0);
+    HIPCHK(hipGetLastError());
+  }
+  if (T.cond) {
+    if (!R.plan) {
+      cat24_kernel<<<cdiv(N * 24, 256), 256, 0, R.st>>>(a.vals, a.mask, T.in24, N);
+      HIPCHK(hipGetLastError());
+    }
+    dense_fwd(R, T.in24, 24, srcp(m, "cond_mlp.0.weight"), srcp(m, "cond_mlp.0.bias"), N, 256, 24, T.ca, 256);
+    if (!R.plan) {
+      silu_fwd_kernel<<<ew_blocks((size_t)N * 256), 256, 0, R.st>>>(T.ca, T.ch, (size_t)N * 256);
+      HIPCHK(hipGetLastError());
+    }
+    dense_fwd(R, T.ch, 256, srcp(m, "cond_mlp.2.weight"), srcp(m, "cond_mlp.2.bias"), N, 256, 256, T.v, 256);
+    if (!R.plan) {
+      add_kernel<<<ew_blocks((size_t)N * 256), 256, 0, R.st>>>(T.v, T.v0, (size_t)N * 256);
+      HIPCHK(hipGetLastError());
+    }
+  } else if (!R.plan) {
+    HIPCHK(hipMemcpyAsync(T.v, T.v0, (size_t)N * 256 * sizeof(float), hipMemcpyDeviceToDevice, R.st));
+  }
+  if (!R.plan) {
+    silu_fwd_kernel<<<ew_blocks((size_t)N * 256), 256, 0, R.st>>>(T.v, T.s, (size_t)N * 256);
+    HIPCHK(hipGetLastError());
+  }
+  int off[6], hc[6];
+  emb_head_slices(m, off, hc);
+  for (int i = 0; i < 6; ++i) {
+    const std::string p = std::string(kEmbHeads[i]) + ".emb_layer.1";
+    dense_fwd(R, T.s, 256, srcp(m, p + ".weight"), srcp(m, p + ".bias"), N, hc[i], 256, T.heads + off[i], m->hsum);
+  }
+  // trunk (models/unet_cond_geom.py:52-76)
+  R.layer = "train.inc";
+  T.inc = train_res(R, m->inc, T.xin, N, H, W, false, nullptr, 0, 0);
+  const float* cur = T.inc.out;
+  int ch = H, cw = W, cc = 64;
+  for (int i = 0; i < 3; ++i) {
+    T.skip[i] = cur;
+    T.sh[i] = ch;
+    T.sw[i] = cw;
+    T.sc[i] = cc;
+    const int nh = ch / 2, nw = cw / 2;
+    T.pooled[i] = R.ws.get<float>((size_t)N * nh * nw * cc);
+    SrcDesc mp = plain_src(cur, cc);
+    mp.Hs = ch;
+    mp.Ws = cw;
+    R.layer = "train.down" + std::to_string(i + 1);
+    prep<SRC_MAXPOOL>(R, mp, T.pooled[i], N, nh, nw, "prep_kernel<2>");
+    T.dr0[i] = train_res(R, m->down[i].r0, T.pooled[i], N, nh, nw, true, nullptr, 0, 0);
+    T.dr1[i] = train_res(R, m->down[i].r1, T.dr0[i].out, N, nh, nw, false, T.heads, m->hsum, m->down[i].emb_off);
+    cc = m->down[i].cout;
+    ch = nh;
+    cw = nw;
+    R.layer = "train.sa" + std::to_string(i + 1);
+    T.dsa[i] = train_attn(R, m->sa[i], T.dr1[i].out, N, ch, cw);
+    cur = T.dsa[i].out;
+  }
+  for (int i = 0; i < m->nbot; ++i) {
+    R.layer = "train.bot" + std::to_string(i + 1);
+    T.bot[i] = train_res(R, m->bot[i], cur, N, ch, cw, false, nullptr, 0, 0);
+    cur = T.bot[i].out;
+    cc = m->bot[i].cout;
+  }
+  for (int i = 0; i < 3; ++i) {
+    const int si = 2 - i;
+    TUp& u = T.up[i];
+    u.skip = T.skip[si];
+    u.low = cur;
+    u.C0 = T.sc[si];
+    u.C1 = cc;
+    u.H = T.sh[si];
+    u.W = T.sw[si];
+    u.Hs = ch;
+    u.Ws = cw;
+    const int dy = u.H - 2 * ch, dx = u.W - 2 * cw;
+    u.padT = dy > 0 ? dy / 2 : 0;
+    u.padL = dx > 0 ? dx / 2 : 0;
+    SrcDesc us = plain_src(u.skip, u.C0 + u.C1);
+    us.C0 = u.C0;
+    us.src1 = cur;
+    us.Hs = ch;
+    us.Ws = cw;
+    us.padT = u.padT;
+    us.padL = u.padL;
+    REQUIRE(us.C == m->up[i].r0.cin, "up: channel mismatch");
+    u.cat = R.ws.get<float>((size_t)N * u.H * u.W * us.C);
+    R.layer = "train.up" + std::to_string(i + 1);
+    prep<SRC_UPCAT>(R, us, u.cat, N, u.H, u.W, "prep_kernel<3>");
+    T.ur0[i] = train_res(R, m->up[i].r0, u.cat, N, u.H, u.W, true, nullptr, 0, 0);
+    T.ur1[i] = train_res(R, m->up[i].r1, T.ur0[i].out, N, u.H, u.W, false, T.heads, m->hsum, m->up[i].emb_off);
+    ch = u.H;
+    cw = u.W;
+    cc = m->up[i].cout;
+    R.layer = "train.sa" + std::to_string(4 + i);
+    T.usa[i] = train_attn(R, m->sa[3 + i], T.ur1[i].out, N, ch, cw);
+    cur = T.usa[i].out;
+  }
+  T.feat = cur;
+  // heads: out conv 1x1 (unet_cond.py:153) and GeomHead GAP -> Linear -> SiLU -> Linear
+  const bool geom = m->kind == DMX_UNET_COND_GEOM;
+  if (geom) {
+    T.g = R.ws.get<float>((size_t)N * 64);
+    T.hpre = R.ws.get<float>((size_t)N * m->cfg.ghid);
+    T.hs = R.ws.get<float>((size_t)N * m->cfg.ghid);
+  }
+  if (R.plan) return;
+  R.layer = "train.heads";
+  out_head_kernel<<<dim3(cdiv(HW, 256), N), 256, 0, R.st>>>(T.feat, m->out_w, m->out_b, a.eps, m->in_ch, HW,
+                                                            m->range_flag);
+  HIPCHK(hipGetLastError());
+  if (geom) {
+    const int gh = m->cfg.ghid;
+    gap_fwd_kernel<<<N, 256, 0, R.st>>>(T.feat, HW, T.g);
+    dense_fwd(R, T.g, 64, srcp(m, "geom_head.mlp.0.weight"), srcp(m, "geom_head.mlp.0.bias"), N, gh, 64, T.hpre, gh);
+    silu_fwd_kernel<<<ew_blocks((size_t)N * gh), 256, 0, R.st>>>(T.hpre, T.hs, (size_t)N * gh);
+    HIPCHK(hipGetLastError());
+    if (a.geom != nullptr)
+      dense_fwd(R, T.hs, gh, srcp(m, "geom_head.mlp.2.weight"), srcp(m, "geom_head.mlp.2.bias"), N, m->cfg.gdim, gh,
+                a.geom, m->cfg.gdim);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// backward building blocks
+// ---------------------------------------------------------------------------
+static void colsum(Run& R, const float* in, int rows, int C, size_t stride, float* out) {
+  if (R.plan) return;
+  colsum_kernel<<<cdiv(C, 256), 256, 0, R.st>>>(in, rows, C, stride, out, 0);
+  HIPCHK(hipGetLastError());
+}
+
+// bias gradient = column sums of dY [M][C] (fixed order: 256-row blocks, then blocks in order)
+static void bias_grad(Run& R, const float* dy, int M, int C, float* out) {
+  const int rpb = 256, nb = cdiv(M, rpb);
+  float* part = R.ws.get<float>((size_t)nb * C);
+  if (R.plan) return;
+  rowsum_part_kernel<<<nb, 256, 0, R.st>>>(dy, M, C, rpb, part);
+  HIPCHK(hipGetLastError());
+  colsum(R, part, nb, C, C, out);
+}
+
+// weight gradient of a conv3x3 (taps 9) / Linear (taps 1) over NHWC input x and NHWC dY
+static void wgrad(Run& R, const float* dy, const float* x, int N, int H, int W, int Cin, int Cout, int taps,
+                  int cin_real, float* grad) {
+  const int M = N * H * W, K = taps * Cin;
+  const int bxy = cdiv(Cout, 64) * cdiv(K, 64);
+  int splits = std::max(1, std::min(cdiv(1024, bxy), cdiv(M, 256)));
+  const int rps = rup(cdiv(M, splits), 16);
+  splits = cdiv(M, rps);
+  float* part = R.ws.get<float>((size_t)splits * Cout * K);
+  if (R.plan) return;
+  WgradParams p{dy, x, N, H, W, Cin, Cout, taps, M, K, rps, part};
+  R.begin("wgrad_kernel", 2.0 * M * (double)Cout * K, 4.0 * ((double)M * (Cout + Cin) + (double)splits * Cout * K));
+  wgrad_kernel<<<dim3(cdiv(Cout, 64), cdiv(K, 64), splits), 256, 0, R.st>>>(p);
+  R.end();
+  HIPCHK(hipGetLastError());
+  wgrad_finish_kernel<<<ew_blocks((size_t)Cout * K), 256, 0, R.st>>>(part, splits, Cout, Cin, cin_real, taps, grad);
+  HIPCHK(hipGetLastError());
+}
+
+// data gradient through a packed transposed / flipped weight: dx (+)= dY * W'
+static void dgrad(Run& R, const float* dy, int Cy, int N, int H, int W, const ConvW& dw, float* dx, bool accumulate) {
+  gemm(R, plain_src(dy, Cy), SRC_PLAIN, N, H, W, dw, accumulate ? EPI_BIAS_RES : EPI_BIAS, dx,
+       accumulate ? dx : nullptr, nullptr, 1);
+}
+
+static void gn_bwd(Run& R, const float* r, const float2* rp, int nseg, int rrows, const Vec& g, const Vec& b,
+                   const float* res, int act, const float* dout, int N, int C, int HW, float* dr, float* dres,
+                   int dres_mode, float* ggamma, float* gbeta, float* demb, int demb_stride, int demb_off) {
+  float* sums = R.ws.get<float>((size_t)2 * N);
+  float* chpart = R.ws.get<float>((size_t)N * 2 * C);
+  if (R.plan) return;
+  GnBwdParams p;
+  std::memset(&p, 0, sizeof(p));
+  p.r = r;
+  p.rowpart = rp;
+  p.nseg = nseg;
+  p.rrows = rrows;
+  p.gamma = g.p;
+  p.beta = b.p;
+  p.res = res;
+  p.act = act;
+  p.dout = dout;
+  p.C = C;
+  p.HW = HW;
+  p.dr = dr;
+  p.dres = dres;
+  p.dres_mode = dres_mode;
+  p.sums = sums;
+  p.chpart = chpart;
+  p.demb = demb;
+  p.demb_stride = demb_stride;
+  p.demb_off = demb_off;
+  R.begin("gn_bwd_reduce_kernel", 0.0, 4.0 * (double)N * HW * C * (res ? 3 : 2));
+  gn_bwd_reduce_kernel<<<N, 256, 0, R.st>>>(p);
+  R.end();
+  HIPCHK(hipGetLastError());
+  const int chunks = std::max(1, std::min(64, cdiv(HW * C, 4096)));
+  R.begin("gn_bwd_apply_kernel", 0.0, 4.0 * (double)N * HW * C * (res ? 4 : 3));
+  gn_bwd_apply_kernel<<<dim3(chunks, N), 256, 0, R.st>>>(p);
+  R.end();
+  HIPCHK(hipGetLastError());
+  colsum(R, chpart, N, C, 2 * (size_t)C, ggamma);
+  colsum(R, chpart + C, N, C, 2 * (size_t)C, gbeta);
+}
+
+static void ln_bwd(Run& R, const float* x, const Vec& w, const float* dy, float* dx, bool accumulate, int M, int C,
+                   float* gw, float* gb) {
+  const int blocks = cdiv(M, 4);
+  float* part = R.ws.get<float>((size_t)blocks * 2 * C);
+  if (R.plan) return;
+  R.begin("ln_bwd_kernel", 0.0, 4.0 * (double)M * C * 3);
+  switch (C) {
+    case 64: ln_bwd_kernel<1><<<blocks, 256, 0, R.st>>>(x, w.p, dy, dx, accumulate ? 1 : 0, part, M); break;
+    case 128: ln_bwd_kernel<2><<<blocks, 256, 0, R.st>>>(x, w.p, dy, dx, accumulate ? 1 : 0, part, M); break;
+    case 256: ln_bwd_kernel<4><<<blocks, 256, 0, R.st>>>(x, w.p, dy, dx, accumulate ? 1 : 0, part, M); break;
+    default: throw Error(DMX_E_INTERNAL, "ln_bwd: unsupported C");
+  }
+  R.end();
+  HIPCHK(hipGetLastError());
+  colsum(R, part, blocks, C, 2 * (size_t)C, gw);
+  colsum(R, part + C, blocks, C, 2 * (size_t)C, gb);
+}
+
+static void attn_core_bwd(Run& R, const float* qkv, const float* o, const float* dout, float* dqkv, int N, int L,
+                          int C) {
+  float* st = R.ws.get<float>((size_t)N * 4 * L * 3);
+  if (R.plan) return;
+  const int D = C / 4;
+  const dim3 grid(cdiv(L, 64), 4, N);
+  R.begin("attn_bwd_kernels<" + std::to_string(D) + ">", 3.0 * 4.0 * N * (double)L * L * C, 4.0 * N * (double)L * 6 * C);
+  if (D == 16) {
+    attn_rowstats_kernel<16><<<grid, 64, 0, R.st>>>(qkv, o, dout, st, L, C);
+    attn_dq_kernel<16><<<grid, 64, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
+    attn_dkv_kernel<16><<<grid, 64, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
+  } else if (D == 32) {
+    attn_rowstats_kernel<32><<<grid, 64, 0, R.st>>>(qkv, o, dout, st, L, C);
+    attn_dq_kernel<32><<<grid, 64, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
+    attn_dkv_kernel<32><<<grid, 64, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
+  } else if (D == 64) {
+    attn_rowstats_kernel<64><<<grid, 64, 0, R.st>>>(qkv, o, dout, st, L, C);
+    attn_dq_kernel<64><<<grid, 64, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
+    attn_dkv_kernel<64><<<grid, 64, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
+  } else {
+    throw Error(DMX_E_INTERNAL, "attention backward: unsupported head dim");
+  }
+  R.end();
+  HIPCHK(hipGetLastError());
+}
+
+// ResBlock backward: dout -> dx (x's gradient; accumulated when dx_acc), parameter gradients,
+// and the emb slice's per-sample sums into demb (Down / Up second block).
+static void res_bwd(Run& R, const TRes& t, const GradMap& G, const float* dout, float* dx, bool dx_acc, float* demb,
+                    int demb_stride) {
+  const ResW& w = *t.w;
+  const int N = t.N, H = t.H, W = t.W, M = N * H * W, HW = H * W, seg = 32;
+  const std::string& p = w.prefix;
+  float* dr2 = R.ws.get<float>((size_t)M * w.cout);
+  gn_bwd(R, t.r2, t.rp2, w.cout / seg, t.rr2, w.g2, w.b2, t.residual ? t.x : nullptr, 0, dout, N, w.cout, HW, dr2,
+         t.residual ? dx : nullptr, t.residual ? (dx_acc ? 2 : 1) : 0, G(p + ".double_conv.4.weight"),
+         G(p + ".double_conv.4.bias"), t.emb_off >= 0 ? demb : nullptr, demb_stride, t.emb_off);
+  wgrad(R, dr2, t.a1, N, H, W, w.mid, w.cout, 9, w.mid, G(p + ".double_conv.3.weight"));
+  float* da1 = R.ws.get<float>((size_t)M * w.mid);
+  dgrad(R, dr2, w.cout, N, H, W, w.d2, da1, false);
+  float* dr1 = R.ws.get<float>((size_t)M * w.mid);
+  gn_bwd(R, t.r1, t.rp1, w.mid / seg, t.rr1, w.g1, w.b1, nullptr, 1, da1, N, w.mid, HW, dr1, nullptr, 0,
+         G(p + ".double_conv.1.weight"), G(p + ".double_conv.1.bias"), nullptr, 0, 0);
+  wgrad(R, dr1, t.x, N, H, W, w.cin, w.mid, 9, w.cin_real, G(p + ".double_conv.0.weight"));
+  if (dx != nullptr) dgrad(R, dr1, w.mid, N, H, W, w.d1, dx, t.residual || dx_acc);
+}
+
+// AttenionBlock backward; dout (the block output's gradient) is consumed (used as scratch).
+static void attn_bwd(Run& R, const TAttn& t, const GradMap& G, float* dout, float* dx) {
+  const AttnW& a = *t.w;
+  const int C = a.c, N = t.N, H = t.H, W = t.W, M = N * H * W, L = H * W;
+  const std::string& p = a.prefix;
+  // out = ff2(gelu(ff1(al))) + av
+  wgrad(R, dout, t.f, N, H, W, C, C, 1, C, G(p + ".ff_self.3.weight"));
+  bias_grad(R, dout, M, C, G(p + ".ff_self.3.bias"));
+  float* dh = R.ws.get<float>((size_t)M * C);
+  dgrad(R, dout, C, N, H, W, a.df2, dh, false);
+  if (!R.plan) {
+    gelu_bwd_kernel<<<ew_blocks((size_t)M * C), 256, 0, R.st>>>(dh, t.h1, dh, (size_t)M * C);
+    HIPCHK(hipGetLastError());
+  }
+  wgrad(R, dh, t.al, N, H, W, C, C, 1, C, G(p + ".ff_self.1.weight"));
+  bias_grad(R, dh, M, C, G(p + ".ff_self.1.bias"));
+  float* dal = R.ws.get<float>((size_t)M * C);
+  dgrad(R, dh, C, N, H, W, a.df1, dal, false);
+  // al = LN2(av): dav = dout + LN2^T(dal)
+  ln_bwd(R, t.av, a.l2w, dal, dout, true, M, C, G(p + ".ff_self.0.weight"), G(p + ".ff_self.0.bias"));
+  float* dav = dout;
+  // av = out_proj(attn(xl)) + xl
+  wgrad(R, dav, t.ao, N, H, W, C, C, 1, C, G(p + ".mha.out_proj.weight"));
+  bias_grad(R, dav, M, C, G(p + ".mha.out_proj.bias"));
+  float* dao = R.ws.get<float>((size_t)M * C);
+  dgrad(R, dav, C, N, H, W, a.dout, dao, false);
+  float* dqkv = R.ws.get<float>((size_t)M * 3 * C);
+  attn_core_bwd(R, t.qkv, t.ao, dao, dqkv, N, L, C);
+  wgrad(R, dqkv, t.xl, N, H, W, C, 3 * C, 1, C, G(p + ".mha.in_proj_weight"));
+  bias_grad(R, dqkv, M, 3 * C, G(p + ".mha.in_proj_bias"));
+  dgrad(R, dqkv, 3 * C, N, H, W, a.dqkv, dav, true);  // dxl = dav + in_proj^T(dqkv)
+  ln_bwd(R, t.x, a.l1w, dav, dx, false, M, C, G(p + ".ln.weight"), G(p + ".ln.bias"));
+}
+
+static void zero_grad(Run& R, const GradMap& G, dmx_model* m, const std::string& name) {
+  if (R.plan) return;
+  for (auto& k : m->keys)
+    if (k.name == name) {
+      size_t n = 1;
+      for (auto s : k.shape) n *= (size_t)s;
+      HIPCHK(hipMemsetAsync(G(name), 0, n * sizeof(float), R.st));
+    }
+}
+
+static void dense_dw(Run& R, const float* dy, int ldy, const float* x, int ldx, int rows, int O, int K, float* dw,
+                     float* db) {
+  if (R.plan) return;
+  dense_dw_kernel<<<cdiv(O * K + O, 256), 256, 0, R.st>>>(dy, ldy, x, ldx, rows, O, K, dw, db);
+  HIPCHK(hipGetLastError());
+}
+static void dense_dx(Run& R, const float* dy, int ldy, const float* w, int rows, int O, int K, float* dx, int ldx,
+                     bool accumulate) {
+  if (R.plan) return;
+  dense_dx_kernel<<<ew_blocks((size_t)rows * K), 256, 0, R.st>>>(dy, ldy, w, rows, O, K, dx, ldx, accumulate ? 1 : 0);
+  HIPCHK(hipGetLastError());
+}
+
+static void train_bwd_body(Run& R, Tape& T, const GradMap& G, const float* d_eps, const float* d_geom) {
+  dmx_model* m = R.m;
+  const int N = T.n, H = T.h, W = T.w, HW = H * W, M = N * HW, Co = m->in_ch;
+  // heads
+  R.layer = "train.heads.bwd";
+  float* dfeat = R.ws.get<float>((size_t)M * 64);
+  float* dyo = R.ws.get<float>((size_t)M * Co);
+  if (!R.plan) {
+    if (d_eps != nullptr) {
+      nchw_to_nhwc_kernel<<<ew_blocks((size_t)M * Co), 256, 0, R.st>>>(d_eps, dyo, N, Co, Co, HW);
+    } else {
+      HIPCHK(hipMemsetAsync(dyo, 0, (size_t)M * Co * sizeof(float), R.st));
+    }
+    HIPCHK(hipGetLastError());
+  }
+  wgrad(R, dyo, T.feat, N, H, W, 64, Co, 1, 64, G("out.weight"));
+  bias_grad(R, dyo, M, Co, G("out.bias"));
+  dense_dx(R, dyo, Co, srcp(m, "out.weight"), M, Co, 64, dfeat, 64, false);
+  if (m->kind == DMX_UNET_COND_GEOM) {
+    const int gh = m->cfg.ghid, gd = m->cfg.gdim;
+    float* dhs = R.ws.get<float>((size_t)N * gh);
+    float* dg = R.ws.get<float>((size_t)N * 64);
+    if (d_geom != nullptr) {
+      dense_dw(R, d_geom, gd, T.hs, gh, N, gd, gh, G("geom_head.mlp.2.weight"), G("geom_head.mlp.2.bias"));
+      dense_dx(R, d_geom, gd, srcp(m, "geom_head.mlp.2.weight"), N, gd, gh, dhs, gh, false);
+      if (!R.plan) {
+        silu_bwd_kernel<<<ew_blocks((size_t)N * gh), 256, 0, R.st>>>(dhs, T.hpre, dhs, (size_t)N * gh, 0);
+        HIPCHK(hipGetLastError());
+      }
+      dense_dw(R, dhs, gh, T.g, 64, N, gh, 64, G("geom_head.mlp.0.weight"), G("geom_head.mlp.0.bias"));
+      dense_dx(R, dhs, gh, srcp(m, "geom_head.mlp.0.weight"), N, gh, 64, dg, 64, false);
+      if (!R.plan) {
+        gap_bwd_kernel<<<ew_blocks((size_t)M * 64), 256, 0, R.st>>>(dg, N, HW, dfeat);
+        HIPCHK(hipGetLastError());
+      }
+    } else {
+      for (const char* k : {"geom_head.mlp.0.weight", "geom_head.mlp.0.bias", "geom_head.mlp.2.weight",
+                            "geom_head.mlp.2.bias"})
+        zero_grad(R, G, m, k);
+    }
+  }
+  float* demb = R.ws.get<float>((size_t)N * m->hsum);
+  float* dskip[3];
+  for (int i = 0; i < 3; ++i) dskip[i] = R.ws.get<float>((size_t)N * T.sh[i] * T.sw[i] * T.sc[i]);
+  // up path, last block first
+  float* dcur = dfeat;
+  for (int i = 2; i >= 0; --i) {
+    const int si = 2 - i;
+    const TUp& u = T.up[i];
+    const int Mi = N * u.H * u.W, Cin = u.C0 + u.C1;
+    R.layer = "train.up" + std::to_string(i + 1) + ".bwd";
+    float* dxs = R.ws.get<float>((size_t)Mi * m->up[i].cout);
+    attn_bwd(R, T.usa[i], G, dcur, dxs);
+    float* dh0 = R.ws.get<float>((size_t)Mi * Cin);
+    res_bwd(R, T.ur1[i], G, dxs, dh0, false, demb, m->hsum);
+    float* dcat = R.ws.get<float>((size_t)Mi * Cin);
+    res_bwd(R, T.ur0[i], G, dh0, dcat, false, nullptr, 0);
+    float* dlow = R.ws.get<float>((size_t)N * u.Hs * u.Ws * u.C1);
+    if (!R.plan) {
+      const size_t tot = (size_t)Mi * u.C0 + (size_t)N * u.Hs * u.Ws * u.C1;
+      upcat_bwd_kernel<<<ew_blocks(tot), 256, 0, R.st>>>(dcat, dskip[si], dlow, N, u.H, u.W, u.C0, u.C1, u.Hs, u.Ws,
+                                                         u.padT, u.padL, 0, 0);
+      HIPCHK(hipGetLastError());
+    }
+    dcur = dlow;
+  }
+  for (int i = m->nbot - 1; i >= 0; --i) {
+    R.layer = "train.bot" + std::to_string(i + 1) + ".bwd";
+    const TRes& b = T.bot[i];
+    float* d = R.ws.get<float>((size_t)b.N * b.H * b.W * b.w->cin);
+    res_bwd(R, b, G, dcur, d, false, nullptr, 0);
+    dcur = d;
+  }
+  for (int i = 2; i >= 0; --i) {
+    R.layer = "train.down" + std::to_string(i + 1) + ".bwd";
+    const TRes& r1 = T.dr1[i];
+    const int Mi = N * r1.H * r1.W, Cin = T.sc[i];
+    float* dxs = R.ws.get<float>((size_t)Mi * m->down[i].cout);
+    attn_bwd(R, T.dsa[i], G, dcur, dxs);
+    float* dh0 = R.ws.get<float>((size_t)Mi * Cin);
+    res_bwd(R, r1, G, dxs, dh0, false, demb, m->hsum);
+    float* dpool = R.ws.get<float>((size_t)Mi * Cin);
+    res_bwd(R, T.dr0[i], G, dh0, dpool, false, nullptr, 0);
+    if (!R.plan) {
+      maxpool_bwd_kernel<<<ew_blocks((size_t)N * T.sh[i] * T.sw[i] * Cin), 256, 0, R.st>>>(
+          T.skip[i], dpool, dskip[i], N, T.sh[i], T.sw[i], Cin, 1);
+      HIPCHK(hipGetLastError());
+    }
+    dcur = dskip[i];
+  }
+  R.layer = "train.inc.bwd";
+  res_bwd(R, T.inc, G, dcur, nullptr, false, nullptr, 0);
+  // embedding
+  R.layer = "train.embed.bwd";
+  float* ds = R.ws.get<float>((size_t)N * 256);
+  float* dv = R.ws.get<float>((size_t)N * 256);
+  int off[6], hc[6];
+  emb_head_slices(m, off, hc);
+  for (int i = 0; i < 6; ++i) {
+    const std::string p = std::string(kEmbHeads[i]) + ".emb_layer.1";
+    dense_dw(R, demb + off[i], m->hsum, T.s, 256, N, hc[i], 256, G(p + ".weight"), G(p + ".bias"));
+    dense_dx(R, demb + off[i], m->hsum, srcp(m, p + ".weight"), N, hc[i], 256, ds, 256, i > 0);
+  }
+  if (!R.plan) {
+    silu_bwd_kernel<<<ew_blocks((size_t)N * 256), 256, 0, R.st>>>(ds, T.v, dv, (size_t)N * 256, 0);
+    class_emb_bwd_kernel<<<m->cfg.ncls, 256, 0, R.st>>>(dv, T.y, N, m->cfg.ncls, G("class_emb.weight"));
+    HIPCHK(hipGetLastError());
+  }
+  if (T.cond) {
+    float* dch = R.ws.get<float>((size_t)N * 256);
+    dense_dw(R, dv, 256, T.ch, 256, N, 256, 256, G("cond_mlp.2.weight"), G("cond_mlp.2.bias"));
+    dense_dx(R, dv, 256, srcp(m, "cond_mlp.2.weight"), N, 256, 256, dch, 256, false);
+    if (!R.plan) {
+      silu_bwd_kernel<<<ew_blocks((size_t)N * 256), 256, 0, R.st>>>(dch, T.ca, dch, (size_t)N * 256, 0);
+      HIPCHK(hipGetLastError());
+    }
+    dense_dw(R, dch, 256, T.in24, 24, N, 256, 24, G("cond_mlp.0.weight"), G("cond_mlp.0.bias"));
+  } else {
+    for (const char* k : {"cond_mlp.0.weight", "cond_mlp.0.bias", "cond_mlp.2.weight", "cond_mlp.2.bias"})
+      zero_grad(R, G, m, k);
+  }
+}
+
+static void check_train(dmx_model* m, int n, int h, int w) {
+  check_shapes(m, n, h, w);
+  REQUIRE(m->kind == DMX_UNET_COND_GEOM || m->kind == DMX_UNET_COND,
+          "training is implemented for UnetCond / UnetCondWithGeomHead");
+}
+
+// Run body with the model in exact-fp32 GEMM mode (restored afterwards).
+template <typename F>
+static void with_fp32(dmx_model* m, F&& f) {
+  const int prec = m->prec;
+  m->prec = 0;
+  try {
+    f();
+  } catch (...) {
+    m->prec = prec;
+    throw;
+  }
+  m->prec = prec;
+}
+
+static void refresh_model(dmx_model* m, hipStream_t st) {
+  if (!m->finalized) throw Error(DMX_E_STATE, "model weights not finalized");
+  for (auto& f : m->jobs) f(st);
+  m->planes_stale = true;
+}
+
+}  // namespace dmx

@@ -89,6 +89,7 @@ class NativeModel:
         h = ctypes.c_void_p()
         conf = _lib.ModelConfig.make(kind, in_ch, remove_deep_conv, **cfg)
         self.geom_dim = int(conf.geom_dim)
+        self.keys = _lib.model_keys(kind, in_ch, remove_deep_conv, **cfg)
         check(self.lib.dmx_model_create_cfg(self.ctx.handle, ctypes.byref(conf), ctypes.byref(h)))
         self.handle = h
         keep = []
@@ -100,7 +101,10 @@ class NativeModel:
                                                 tt.dim()))
         with torch.cuda.device(self.device):
             check(self.lib.dmx_model_finalize(self.handle, ctypes.c_void_p(_stream(self.device))))
-        del keep
+        # the registered tensors (views of the module's fp32 parameters, or converted copies) are
+        # re-read by refresh() and the training entry points (include/dmx.h dmx_model_set_tensor)
+        self._registered = keep
+        self.aliases_params = all(k.data_ptr() == p.data_ptr() for k, p in zip(keep, params.values()))
         self._side_stream = None
         env = os.environ.get("DMX_PRECISION")
         if env:
@@ -145,6 +149,50 @@ class NativeModel:
                 self.handle = None
         except Exception:
             pass
+
+    def refresh(self) -> None:
+        """Parameters changed in place (optimizer.step / load_state_dict): repack on the device."""
+        with torch.cuda.device(self.device):
+            check(self.lib.dmx_model_refresh(self.handle, ctypes.c_void_p(_stream(self.device))))
+
+    # ---- training (include/dmx.h dmx_train_forward / dmx_train_backward) --------------------
+    def train_forward(self, x, t, y, vals=None, mask=None):
+        """Forward with a tape for dmx_train_backward -> (eps, geom or None, tape id)."""
+        require_cuda(x, "x")
+        n, c, h, w = x.shape
+        dev = x.device
+        self.ctx.ensure_time_table(max(1000, int(t.max().item()) if t.numel() else 1))
+        x = x.detach().to(dtype=torch.float32).contiguous()
+        t = t.to(device=dev, dtype=torch.long).contiguous()
+        y = y.to(device=dev, dtype=torch.long).contiguous()
+        if vals is not None:
+            vals = vals.detach().to(device=dev, dtype=torch.float32).contiguous()
+            mask = mask.detach().to(device=dev, dtype=torch.float32).contiguous()
+        eps = torch.empty_like(x)
+        geom = (torch.empty((n, self.geom_dim), device=dev, dtype=torch.float32)
+                if self.kind == _lib.DMX_UNET_COND_GEOM else None)
+        tid = ctypes.c_int64()
+        with torch.cuda.device(dev):
+            check(self.lib.dmx_train_forward(self.handle, _ptr(x), _ptr(t), _ptr(y), _ptr(vals), _ptr(mask), n, h, w,
+                                             _ptr(eps), _ptr(geom), ctypes.byref(tid),
+                                             ctypes.c_void_p(_stream(dev))))
+        self._live_train = (x, t, y, vals, mask)
+        return eps, geom, int(tid.value)
+
+    def train_backward(self, tape_id: int, d_eps=None, d_geom=None) -> Dict[str, torch.Tensor]:
+        """dLoss/dparam for every state_dict key, given dLoss/deps and dLoss/dgeom (None = 0)."""
+        dev = self.device
+        grads = {name: torch.empty(shape, device=dev, dtype=torch.float32) for name, shape in self.keys}
+        ptrs = (ctypes.c_void_p * len(self.keys))(*[grads[name].data_ptr() for name, _ in self.keys])
+        if d_eps is not None:
+            d_eps = d_eps.to(device=dev, dtype=torch.float32).contiguous()
+        if d_geom is not None:
+            d_geom = d_geom.to(device=dev, dtype=torch.float32).contiguous()
+        with torch.cuda.device(dev):
+            check(self.lib.dmx_train_backward(self.handle, int(tape_id), _ptr(d_eps), _ptr(d_geom), ptrs,
+                                              len(self.keys), ctypes.c_void_p(_stream(dev))))
+        self._live_bwd = (d_eps, d_geom)
+        return grads
 
     def workspace_bytes(self) -> int:
         return int(self.lib.dmx_model_workspace_bytes(self.handle))

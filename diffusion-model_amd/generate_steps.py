@@ -243,10 +243,9 @@ def save_reverse_steps_for_csv_row(
             if device_loop:  # one graph-replayed step, t decremented on the device
                 t_dev.fill_(i)
                 nm.sample_loop(x, t_dev, y, null_label, v, m, float(guidance_scale), tables, 1, seed=seed)
-            else:  # generate_steps.py:179-189
+            else:  # generate_steps.py:179-189 (i in [1, T]: denoise_cond's range assert holds)
                 t = torch.full((B,), i, device=device_t, dtype=torch.long)
-                x = diffuser.denoise_cond(model_noise, x, t, y=y, guidance_scale=guidance_scale,
-                                          null_label=null_label, cond_vals=vals, cond_mask=mask)
+                x = diffuser._denoise_cond(model_noise, x, t, y, guidance_scale, null_label, vals, mask)
             if bar is not None:
                 bar.update(1)
         return x.clone() if device_loop else x  # the guard keeps the chunk's input for a replay

@@ -42,15 +42,28 @@ class UnetCond(NativeBacked):
         if not 1 <= self._dmx_in_ch <= 4:
             raise NotImplementedError(f"dmx implements in_ch in [1, 4] (got {self._dmx_in_ch})")
 
-    def _check_training(self, cond_drop_prob=None):
-        p = self.cfg_drop_prob if cond_drop_prob is None else cond_drop_prob
-        if self.training and (self.cfg_drop_prob > 0 or (p or 0) > 0) and type(self) is UnetCond:
-            # models/unet_cond.py:199-211: random CFG label/cond dropout is a training-time feature
-            raise NotImplementedError("training-mode CFG dropout is out of scope for dmx; call .eval()")
+    def _cfg_dropout(self, y, cond_vals, cond_mask, cond_drop_prob):
+        """models/unet_cond.py:199-211: training-mode label / condition dropout, drawn from the
+        global generator in the reference's order (plain torch on the (B,) labels and (B, 12) rows)."""
+        if self.training and self.cfg_drop_prob > 0:
+            drop = torch.rand_like(y.float()) < self.cfg_drop_prob
+            y = torch.where(drop, torch.zeros_like(y), y)
+        if cond_vals is not None and cond_mask is not None:
+            p = self.cfg_drop_prob if cond_drop_prob is None else cond_drop_prob
+            if self.training and p > 0.0:
+                keep = (torch.rand(cond_vals.size(0), device=cond_vals.device) > p).float().unsqueeze(1)
+                cond_vals = cond_vals * keep
+                cond_mask = cond_mask * keep
+        return y, cond_vals, cond_mask
+
+    def _run(self, x, t, y, vals, mask, want_geom=False):
+        if self._dmx_training():
+            return self._dmx_train_forward(x, t, y, vals, mask)
+        return self.native().forward(x, t, y, vals, mask, want_geom=want_geom)
 
     def forward(self, x: torch.Tensor, t: torch.Tensor, y: torch.Tensor, cond_vals: torch.Tensor = None,
                 cond_mask: torch.Tensor = None, cond_drop_prob: float = None):
-        self._check_training(cond_drop_prob)
+        y, cond_vals, cond_mask = self._cfg_dropout(y, cond_vals, cond_mask, cond_drop_prob)
         use = cond_vals is not None and cond_mask is not None  # models/unet_cond.py:205
-        eps, _ = self.native().forward(x, t, y, cond_vals if use else None, cond_mask if use else None)
+        eps, _ = self._run(x, t, y, cond_vals if use else None, cond_mask if use else None)
         return eps

@@ -25,6 +25,5 @@ class UnetCondWithGeomHead(UnetCond):
 
     def forward(self, x: torch.Tensor, t: torch.Tensor, y: torch.Tensor, cond_vals: torch.Tensor = None,
                 cond_mask: torch.Tensor = None, cond_drop_prob: float = 0.0):
-        use = cond_vals is not None and cond_mask is not None  # unet_cond_geom.py:91
-        return self.native().forward(x, t, y, cond_vals if use else None, cond_mask if use else None,
-                                     want_geom=True)
+        use = cond_vals is not None and cond_mask is not None  # unet_cond_geom.py:91 (no dropout here)
+        return self._run(x, t, y, cond_vals if use else None, cond_mask if use else None, want_geom=True)

@@ -84,10 +84,16 @@ int dmx_model_cfg_num_keys(const dmx_model_config* cfg);
 int dmx_model_cfg_key(const dmx_model_config* cfg, int index, char* name_out, int name_cap,
                       int64_t* shape_out /* [4] */, int* ndim_out);
 int dmx_model_destroy(dmx_model* m);
-/* Register one reference-layout tensor (device pointer, fp32 contiguous). */
+/* Register one reference-layout tensor (device pointer, fp32 contiguous).  The pointer is
+ * read by dmx_model_finalize and again by dmx_model_refresh and the training entry points, so
+ * a caller using those keeps the tensor alive (and at the same address) for the model's life. */
 int dmx_model_set_tensor(dmx_model* m, const char* name, const float* dev_ptr, const int64_t* shape, int ndim);
 /* Repack every registered tensor into the model's kernel layouts (device-side). */
 int dmx_model_finalize(dmx_model* m, void* stream);
+/* The registered tensors changed in place (optimizer.step, load_state_dict's copy_): repeat
+ * every repack on `stream` (no host sync); the split-precision planes are re-derived before the
+ * next mode-1/2 launch.  Replaces re-running Utils.loadModel after each update (utils.py:68-73). */
+int dmx_model_refresh(dmx_model* m, void* stream);
 /* GEMM arithmetic: 0 = fp32 MFMA (exact fp32 products), 1 (default) = fp32 operands split
  * into fp16 hi+lo on the fp16 matrix cores (3 MFMAs, fp32 accumulate, ~1e-7 relative),
  * 2 = fp16 operands (BASELINE config 4: one MFMA, fp32 accumulate, fp32 norms/softmax/scheduler). */
@@ -168,6 +174,23 @@ int dmx_eval_metrics(const uint8_t* gt, const uint8_t* pred, int n, int h, int w
  * (VAE.encode's returned kl is kl.mean()). */
 int dmx_vae_encode(dmx_model* m, const float* x, const float* eps, float* z, float* kl, int n, int h, int w,
                    void* stream);
+
+/* ---- training step (replaces the forward + loss.backward() of UnetCondWithGeomHead / UnetCond
+ * in train_latent_cond.py:148-162) ------------------------------------
+ * dmx_train_forward: model(x, t, y, cond_vals, cond_mask) in exact fp32 (mode 0 GEMMs whatever
+ * the model's precision), recording the activations the backward needs in a tape owned by the
+ * model; x: (n,in_ch,h,w); t, y: (n,) int64 (t in [1, tmax], y in [0, num_classes]);
+ * vals/mask: (n,12) or NULL; eps: (n,in_ch,h,w) out; geom: (n,geom_dim) out or NULL.
+ * *tape_id identifies the tape (one per model: a later forward replaces it).
+ * dmx_train_backward: d_eps (n,in_ch,h,w) = dLoss/deps, d_geom (n,geom_dim) = dLoss/dgeom
+ * (either may be NULL = zero); writes dLoss/dparam for every state_dict key into grads[i]
+ * (one device pointer per key in dmx_model_cfg_key order, each of that key's shape; keys whose
+ * branch did not run — cond_mlp without vals — receive zeros).  No gradient for x. */
+int dmx_train_forward(dmx_model* m, const float* x, const int64_t* t, const int64_t* y, const float* vals,
+                      const float* mask, int n, int h, int w, float* eps, float* geom, int64_t* tape_id,
+                      void* stream);
+int dmx_train_backward(dmx_model* m, int64_t tape_id, const float* d_eps, const float* d_geom, float* const* grads,
+                       int n_grads, void* stream);
 
 /* ---- measurement: one eager step with a HIP event pair around every launch -----------
  * Fills up to `cap` records (kernel name as rocprofv3 shows it, layer label, algorithmic

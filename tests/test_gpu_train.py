@@ -1,0 +1,150 @@
+"""The native training step (include/dmx.h dmx_train_forward / dmx_train_backward) driven the
+way train_latent_cond.py:136-163 drives the reference: drop-in module in train mode,
+F.mse_loss (+ masked_geom_mse), loss.backward(), torch Adam.  Checked against the reference's
+own gradients / Adam steps (tests/golden/train_step.npz) and against the CPU oracle's full
+gradient tensors (oracle/train_ref.py).  Tolerances: fp32 arithmetic on both sides, different
+summation orders — per-tensor relative L2 of the gradient <= 1e-4 vs the oracle, the reference
+statistics within 2e-4 of each tensor's L2 norm."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+if HERE not in sys.path:
+    sys.path.insert(0, HERE)
+
+from test_train_oracle import GOLD, case_inputs, case_weights, grad_stats_close  # noqa: E402
+
+
+def _model(tag, dev):
+    from models.unet_cond import UnetCond
+    from models.unet_cond_geom import UnetCondWithGeomHead
+    sd, geom, shallow = case_weights(tag)
+    m = UnetCondWithGeomHead() if geom else UnetCond(cfg_drop_prob=0.0, remove_deep_conv=True)
+    m.load_state_dict(sd)
+    return m.to(dev).train(), geom
+
+
+def _loss(m, geom, inputs, dev, lam):
+    from losses.geom_losses import masked_geom_mse
+    x, t, y, vals, mask, noise, gt = (v.to(dev) if v is not None else None for v in inputs)
+    out = m(x, t, y, cond_vals=vals, cond_mask=mask) if vals is not None else m(x, t, y)
+    eps, g = out if isinstance(out, tuple) else (out, None)
+    loss = F.mse_loss(eps, noise)
+    if g is not None:
+        loss = loss + lam * masked_geom_mse(g, gt, mask)
+    return loss, eps, g
+
+
+@pytest.mark.parametrize("tag", ["g", "c"])
+def test_native_step_matches_reference_and_oracle(cuda, tag):
+    from oracle import train_ref
+    m, geom = _model(tag, cuda)
+    lam = float(GOLD[f"{tag}_lam"])
+    loss, eps, g = _loss(m, geom, case_inputs(tag), cuda, lam)
+    m.zero_grad(set_to_none=True)
+    loss.backward()
+    names = [n for n, _ in m.named_parameters()]
+    grads = {n: p.grad for n, p in m.named_parameters()}
+    assert abs(float(loss) - float(GOLD[f"{tag}_loss"])) <= 2e-5 * float(GOLD[f"{tag}_loss"])
+    np.testing.assert_allclose(eps.detach().cpu().numpy(), GOLD[f"{tag}_eps"], rtol=1e-4, atol=2e-5)
+    if geom:
+        np.testing.assert_allclose(g.detach().cpu().numpy(), GOLD[f"{tag}_geom"], rtol=1e-4, atol=2e-5)
+    assert grad_stats_close(tag, grads, names) == []
+    # full tensors vs the oracle's autograd
+    sd, geom_, shallow = case_weights(tag)
+    x, t, y, vals, mask, noise, gt = case_inputs(tag)
+    _, _, _, ref = train_ref.loss_and_grads(sd, x, t, y, vals, mask, noise, gt, mask, lam, geom_, shallow)
+    worst = []
+    for n in names:
+        if ref[n] is None:
+            assert grads[n] is None, n
+            continue
+        a, b = grads[n].detach().double().cpu(), ref[n].double()
+        worst.append((float((a - b).norm() / max(float(b.norm()), 1e-30)), n))
+    worst.sort(reverse=True)
+    print("[train] worst rel-L2 vs oracle:", worst[:5])
+    assert worst[0][0] <= 1e-4, worst[:5]
+
+
+def test_two_adam_steps_match_reference(cuda):
+    tag = "g"
+    m, geom = _model(tag, cuda)
+    lam = float(GOLD[f"{tag}_lam"])
+    opt = torch.optim.Adam(m.parameters(), lr=1e-4)
+    for second in (False, True):
+        loss, _, _ = _loss(m, geom, case_inputs(tag, second), cuda, lam)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+    names = [n for n, _ in m.named_parameters()]
+    ps = dict(m.named_parameters())
+    idx, after = GOLD[f"{tag}_idx"], GOLD[f"{tag}_p_after"]
+    got = np.stack([ps[n].detach().cpu().reshape(-1)[torch.from_numpy(i)].numpy() for n, i in zip(names, idx)])
+    d = np.abs(got - after)
+    assert d.max() <= 2.1e-4
+    assert (d <= 1e-6 + 1e-5 * np.abs(after)).mean() >= 0.97
+
+
+def test_refresh_after_optimizer_step_equals_fresh_model(cuda):
+    """optimizer.step() changes the parameters in place: the next inference forward repacks on the
+    device (dmx_model_refresh) and must equal a model built from scratch from the same weights."""
+    from models.unet_cond_geom import UnetCondWithGeomHead
+    m, geom = _model("g", cuda)
+    nm0 = m.native()
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    loss, _, _ = _loss(m, geom, case_inputs("g"), cuda, 0.5)
+    opt.zero_grad()
+    loss.backward()
+    opt.step()
+    x, t, y, vals, mask, _, _ = (v.to(cuda) if v is not None else None for v in case_inputs("g"))
+    m.eval()
+    with torch.no_grad():
+        e1, g1 = m(x, t, y, cond_vals=vals, cond_mask=mask)
+    assert m.native() is nm0  # refreshed, not rebuilt
+    fresh = UnetCondWithGeomHead().to(cuda).eval()
+    fresh.load_state_dict(m.state_dict())
+    with torch.no_grad():
+        e2, g2 = fresh(x, t, y, cond_vals=vals, cond_mask=mask)
+    assert torch.equal(e1, e2) and torch.equal(g1, g2)
+
+
+def test_stale_tape_is_refused(cuda):
+    from dmx import _lib
+    m, geom = _model("g", cuda)
+    inputs = case_inputs("g")
+    l1, _, _ = _loss(m, geom, inputs, cuda, 0.5)
+    l2, _, _ = _loss(m, geom, inputs, cuda, 0.5)
+    with pytest.raises(_lib.DmxError, match="stale tape"):
+        l1.backward()
+    l2.backward()  # the current tape still works
+    assert all(p.grad is not None for n, p in m.named_parameters())
+
+
+def test_input_gradients_are_refused(cuda):
+    m, geom = _model("g", cuda)
+    x, t, y, vals, mask, _, _ = (v.to(cuda) if v is not None else None for v in case_inputs("g"))
+    with pytest.raises(NotImplementedError):
+        m(x.requires_grad_(True), t, y, cond_vals=vals, cond_mask=mask)
+
+
+def test_unetcond_training_dropout_draws_like_reference(cuda):
+    """UnetCond.forward in train mode with cfg_drop_prob > 0 draws torch.rand_like(y.float()) then
+    torch.rand(B) for the condition (models/unet_cond.py:199-211) from the global generator."""
+    from models.unet_cond import UnetCond
+    m = UnetCond(cfg_drop_prob=0.5).to(cuda).train()
+    x, t, y, vals, mask, _, _ = (v.to(cuda) if v is not None else None for v in case_inputs("g"))
+    torch.manual_seed(5)
+    with torch.no_grad():
+        m(x, t, y, cond_vals=vals, cond_mask=mask)
+    after = torch.cuda.get_rng_state(cuda)
+    torch.manual_seed(5)
+    torch.rand_like(y.float())
+    torch.rand(vals.size(0), device=cuda)
+    assert torch.equal(after, torch.cuda.get_rng_state(cuda))

@@ -11,6 +11,9 @@ from collections import defaultdict
 
 
 def short(name):
+    m = re.match(r"^_ZN3dmx\d+(\w+?)ILi(\d+)EE", name)  # rocprofv3 leaves some templates mangled (_Float16 args)
+    if m:
+        return f"{m.group(1)}<{m.group(2)}>"
     name = re.sub(r"^void\s+", "", name)
     name = re.sub(r"^dmx::", "", name)
     return re.sub(r"\(.*\)$", "", name).strip()
