@@ -27,6 +27,7 @@ for _p in (os.path.join(REPO, "diffusion-model_amd"), REPO):
         sys.path.insert(0, _p)
 
 import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X dense fp32 MFMA (MI355X_MICROARCH.md, chip table)
 F16_MFMA_PEAK_TFLOPS = 2500.0   # MI355X dense fp16/bf16 MFMA (spec, no sparsity)
@@ -53,6 +54,8 @@ def parse():
                     help="steps timed in BASELINE config 4 (fp16 arithmetic) beside the headline (0 = skip)")
     ap.add_argument("--legs-steps", type=int, default=30,
                     help="steps timed for the fp32-MFMA and host-noise legs beside the headline (0 = skip)")
+    ap.add_argument("--train-steps", type=int, default=10, help="training-step leg (0 = skip)")
+    ap.add_argument("--train-batch", type=int, default=32)
     ap.add_argument("--png-steps", type=int, default=100,
                     help="steps of the generate_steps drop-in (async PNG pipeline) timed for config 5 (0 = skip)")
     return ap.parse_args()
@@ -169,6 +172,87 @@ def legs(nm, model, x, y, vals, mask, args, tables, seed):
                          "path": "Diffuser.sample_latent_cond loop: eager dmx_step per step, noise from torch's CPU "
                                  "generator in the reference's draw order (helper-thread draws, pinned async H2D)"}
     return out
+
+
+def train_leg(args, dev):
+    """The training step of train_latent_cond.py:114-163 on the drop-ins, B = 32 224x224 synthetic
+    images: frozen VAE encode (micro-batches of 8, no_grad), t ~ U{1..1000}, add_noise, CFG dropout
+    (p = 0.1), UnetCondWithGeomHead forward + F.mse_loss + geom_lambda * masked_geom_mse, backward
+    (native dmx_train_backward), torch Adam(lr=1e-4) step.  Also the native forward + backward alone."""
+    import diff
+    from dmx import synth
+    from losses.geom_losses import masked_geom_mse
+    from models.unet_cond_geom import UnetCondWithGeomHead
+    from models.vae import VAE
+    B = args.train_batch
+    g = torch.Generator().manual_seed(7)
+    model = UnetCondWithGeomHead()
+    model.load_state_dict(synth.unet_cond_geom_weights(0))
+    model.to(dev).train()
+    vae = VAE()
+    vae.load_state_dict(synth.vae_weights(1))
+    vae.to(dev).eval()
+    for p in vae.parameters():
+        p.requires_grad = False
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    diffuser = diff.Diffuser(1000, device=dev)
+    images = torch.rand((B, 3, 224, 224), generator=g).to(dev)
+    vals = torch.rand((B, 12), generator=g).to(dev)
+    mask = (torch.rand((B, 12), generator=g) > 0.3).float().to(dev)
+    classes = torch.randint(1, 4, (B,), generator=g).to(dev)
+
+    def step():
+        with torch.no_grad():
+            z = torch.cat([vae.encode(mb)[0] for mb in images.split(8, dim=0)], dim=0)
+        t = torch.randint(1, 1001, (B,), device=dev)
+        z_noisy, noise = diffuser.add_noise(z, t)
+        drop = torch.rand(B, device=dev) < 0.1
+        y_used = torch.where(drop, torch.zeros_like(classes), classes)
+        keep = (~drop).float().unsqueeze(1)
+        eps, geom = model(z_noisy, t, y_used, cond_vals=vals * keep, cond_mask=mask * keep)
+        loss = F.mse_loss(eps, noise) + 0.5 * masked_geom_mse(geom, vals, mask * keep)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    k = args.train_steps
+    t0 = time.perf_counter()
+    for _ in range(k):
+        loss = step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / k
+    assert torch.isfinite(loss), "non-finite training loss"
+    # native forward + backward alone (same shapes)
+    nm = model.native()
+    z = torch.randn((B, 4, 28, 28), generator=g).to(dev)
+    t = torch.randint(1, 1001, (B,), generator=g).to(dev)
+    d_eps, d_geom = torch.randn_like(z), torch.randn((B, nm.geom_dim), device=dev)
+    for _ in range(2):
+        _, _, tape = nm.train_forward(z, t, classes, vals, mask)
+        nm.train_backward(tape, d_eps, d_geom)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        _, _, tape = nm.train_forward(z, t, classes, vals, mask)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(k):
+        _, _, tape = nm.train_forward(z, t, classes, vals, mask)
+        nm.train_backward(tape, d_eps, d_geom)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    fwd = (t1 - t0) / k
+    fb = (t2 - t1) / k
+    return {"value": round(B / dt, 2), "unit": "training images/s (B=%d, 224x224 -> 28x28x4 latents)" % B,
+            "ms_per_step": round(dt * 1e3, 3), "steps": k,
+            "native_forward_ms": round(fwd * 1e3, 3), "native_backward_ms": round((fb - fwd) * 1e3, 3),
+            "dtype": "f32 (exact fp32 MFMA GEMMs, fp32 everywhere)",
+            "path": "train_latent_cond.py step on the drop-ins: VAE.encode x4, add_noise, forward, mse + "
+                    "masked_geom_mse, loss.backward() (dmx_train_backward), torch Adam"}
 
 
 MFMA_FAMILIES = ("igemm_x3_kernel", "igemm_x3g_kernel", "igemm_pp_kernel", "igemm_ad_kernel", "igemm_f32_kernel",
@@ -406,6 +490,8 @@ def main():
         out["config5"] = config5(nm, args, tables, seed)
     if world == 1 and args.legs_steps > 0:
         out.update(legs(nm, model, x, y, vals, mask, args, tables, seed))
+    if world == 1 and args.train_steps > 0:
+        out["train_step"] = train_leg(args, dev)
     if rank == 0:
         if not args.no_profile:
             xp = x.clone()

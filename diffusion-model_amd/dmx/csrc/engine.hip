@@ -211,12 +211,28 @@ struct Arena {
   char* base = nullptr;
   size_t cap = 0, off = 0;
   bool plan = true;
+  // DMX_CHECK: allocation sizes of the plan pass, compared one by one in the real pass
+  std::vector<size_t>* trace = nullptr;
+  size_t n = 0;
+  const std::string* layer = nullptr;
   template <typename T>
   T* get(size_t count) {
     const size_t bytes = (count * sizeof(T) + 255) & ~(size_t)255;
+    if (trace != nullptr) {
+      if (plan) {
+        trace->push_back(bytes);
+      } else if (n >= trace->size() || (*trace)[n] != bytes) {
+        throw std::runtime_error("workspace allocation " + std::to_string(n) + " differs between plan and run (" +
+                                 std::to_string(n < trace->size() ? (*trace)[n] : 0) + " vs " +
+                                 std::to_string(bytes) + " bytes, layer '" + (layer ? *layer : std::string()) + "')");
+      }
+      ++n;
+    }
     char* p = base + off;
     off += bytes;
-    return reinterpret_cast<T*>(plan ? nullptr : p);
+    // plan pass: a non-null placeholder, so code that tests a buffer pointer for null takes the
+    // same branch (and allocates the same) in both passes; it is never dereferenced
+    return reinterpret_cast<T*>(plan ? reinterpret_cast<char*>(static_cast<uintptr_t>(4096) + off) : p);
   }
 };
 
@@ -246,6 +262,7 @@ struct dmx_model {
   dmx::Keys keys;
   std::map<std::string, std::pair<const float*, std::vector<int64_t>>> inputs;
   std::vector<void*> owned;
+  std::map<const char*, size_t> owned_bytes;  // DMX_CHECK operand-range validation
   // U-Net
   dmx::ResW inc, bot[3];
   int nbot = 0;
@@ -355,6 +372,7 @@ struct Packer {
     void* p = nullptr;
     HIPCHK(hipMalloc(&p, n * sizeof(float) + 256));
     m->owned.push_back(p);
+    m->owned_bytes[static_cast<const char*>(p)] = n * sizeof(float) + 256;
     return static_cast<float*>(p);
   }
   // Run a packing step now and record it for dmx_model_refresh.
@@ -683,6 +701,39 @@ struct Deferred {
   const float* bias = nullptr;
 };
 
+// Diagnostic (DMX_CHECK=1): before every implicit-GEMM launch, verify that each operand range
+// lies inside one allocation the model owns (packed weights, workspaces) and throw otherwise —
+// an out-of-range operand is reported on the host instead of faulting the GPU.
+static bool check_args() {
+  static const bool v = [] {
+    const char* e = std::getenv("DMX_CHECK");
+    return e != nullptr && std::atoi(e) != 0;
+  }();
+  return v;
+}
+static void check_range(Run& R, const void* p, size_t bytes, const char* what) {
+  if (!check_args() || p == nullptr || bytes == 0) return;
+  const char* a = static_cast<const char*>(p);
+  const dmx_model* m = R.m;
+  auto inside = [&](const void* base, size_t cap) {
+    const char* b = static_cast<const char*>(base);
+    return base != nullptr && a >= b && a + bytes <= b + cap;
+  };
+  if (inside(m->ws_mem, m->ws_cap) || inside(m->tws_mem, m->tws_cap) || inside(m->bws_mem, m->bws_cap)) return;
+  auto it = m->owned_bytes.upper_bound(a);
+  if (it != m->owned_bytes.begin()) {
+    --it;
+    if (a >= it->first && a + bytes <= it->first + it->second) return;
+  }
+  char msg[512];
+  std::snprintf(msg, sizeof msg,
+                "DMX_CHECK: %s operand [%p, +%zu) of layer '%s' lies outside every model allocation "
+                "(ws %p +%zu, tws %p +%zu, bws %p +%zu, arena off %zu)",
+                what, p, bytes, R.layer.c_str(), m->ws_mem, m->ws_cap, m->tws_mem, m->tws_cap, m->bws_mem, m->bws_cap,
+                R.ws.off);
+  throw Error(DMX_E_INTERNAL, msg);
+}
+
 static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, const ConvW& cw, int epi, float* out,
                 const float* res, float2* rowpart, int seg, const _Float16* ash = nullptr,
                 const _Float16* asl = nullptr, Deferred* defer = nullptr) {
@@ -747,6 +798,17 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   if (x3 && cw.cin < bk) throw Error(DMX_E_INTERNAL, "gemm: x3 path needs Cin >= K-step");
   if (ash != nullptr && !x3) throw Error(DMX_E_INTERNAL, "gemm: f16-plane operand needs the split GEMM");
   if (src_mode != SRC_PLAIN && src_mode != SRC_NCHW) throw Error(DMX_E_INTERNAL, "gemm: unsupported source");
+  if (check_args()) {
+    if (src_mode == SRC_PLAIN)
+      check_range(R, s.src0, (size_t)N * p.Hin * p.Win * s.C * 4, "A");
+    check_range(R, ash, (size_t)N * p.Hin * p.Win * s.C * 2, "A hi");
+    check_range(R, asl, (size_t)N * p.Hin * p.Win * s.C * 2, "A lo");
+    check_range(R, cw.B, (size_t)cw.phases * cw.npad * cw.kpad * 4, "B");
+    check_range(R, partial, (size_t)splits * M * cw.cout * 4, "partial");
+    if (!(splits > 1 && defer != nullptr && defer->fused))
+      check_range(R, out, (size_t)N * p.Hout * p.Wout * cw.cout * 4, "out");
+    check_range(R, res, (size_t)N * p.Hout * p.Wout * cw.cout * 4, "res");
+  }
   X3Params xp;
   xp.g = p;
   xp.Ash = ash;
@@ -1266,6 +1328,20 @@ static void ensure_planes(dmx_model* m, hipStream_t st) {
   m->planes_stale = false;
 }
 
+// Diagnostic (DMX_POISON=1): fill every workspace with 0xFF bytes (fp32 NaN) before the real
+// pass, so a kernel reading an element no earlier kernel of the same run wrote turns the
+// outputs non-finite instead of silently reusing stale data.
+static bool poison_ws() {
+  static const bool v = [] {
+    const char* e = std::getenv("DMX_POISON");
+    return e != nullptr && std::atoi(e) != 0;
+  }();
+  return v;
+}
+static void poison(void* mem, size_t bytes, hipStream_t st) {
+  if (poison_ws() && mem != nullptr && bytes > 0) HIPCHK(hipMemsetAsync(mem, 0xFF, bytes, st));
+}
+
 static void ensure_ws(dmx_model* m) {
   if (m->ws.off > m->ws_cap) {
     if (m->ws_mem) HIPCHK(hipFree(m->ws_mem));
@@ -1291,11 +1367,14 @@ static void run_planned(dmx_model* m, hipStream_t st, F&& body) {
     body(R);
   }
   ensure_ws(m);
+  const size_t planned = m->ws.off;
+  poison(m->ws_mem, m->ws.off, st);
   m->ws.base = static_cast<char*>(m->ws_mem);
   m->ws.off = 0;
   m->ws.plan = false;
   Run R{m, st, false, m->ws};
   body(R);
+  if (m->ws.off != planned) throw Error(DMX_E_INTERNAL, "workspace plan / run mismatch");
 }
 
 static void step_body(Run& R, const dmx_step_args& a) {
@@ -1797,6 +1876,7 @@ int dmx_sample_loop(dmx_model* m, const dmx_step_args* a, int steps, int use_gra
         step_body(P, *a);
       }
       ensure_ws(m);
+      poison(m->ws_mem, m->ws.off, st);
       m->ws.base = static_cast<char*>(m->ws_mem);
       m->ws.off = 0;
       m->ws.plan = false;

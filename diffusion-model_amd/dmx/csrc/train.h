@@ -584,7 +584,7 @@ __global__ __launch_bounds__(64) void attn_dkv_kernel(const float* qkv, const fl
 // ---------------------------------------------------------------------------
 static __global__ void dense_dw_kernel(const float* dy, int ldy, const float* x, int ldx, int R, int O, int K,
                                        float* dw, float* db) {
-  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // grid covers O * K + O
   if (i < (size_t)O * K) {
     const int o = (int)(i / K), k = (int)(i % K);
     float s = 0.f;
@@ -600,23 +600,23 @@ static __global__ void dense_dw_kernel(const float* dy, int ldy, const float* x,
 // dX[r][k] (+)= sum_o dY[r][o] W[o][k]  (W row-major [O][K])
 static __global__ void dense_dx_kernel(const float* dy, int ldy, const float* w, int R, int O, int K, float* dx, int ldx,
                                        int accumulate) {
-  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (size_t)R * K) return;
-  const int r = (int)(i / K), k = (int)(i % K);
-  float s = 0.f;
-  for (int o = 0; o < O; ++o) s += dy[(size_t)r * ldy + o] * w[(size_t)o * K + k];
-  float* d = dx + (size_t)r * ldx + k;
-  *d = accumulate ? *d + s : s;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < (size_t)R * K; i += (size_t)gridDim.x * 256) {
+    const int r = (int)(i / K), k = (int)(i % K);
+    float s = 0.f;
+    for (int o = 0; o < O; ++o) s += dy[(size_t)r * ldy + o] * w[(size_t)o * K + k];
+    float* d = dx + (size_t)r * ldx + k;
+    *d = accumulate ? *d + s : s;
+  }
 }
 // y = x W^T + b (forward for the small layers of the training tape)
 static __global__ void dense_fwd_kernel(const float* x, int ldx, const float* w, const float* b, int R, int O, int K,
                                         float* y, int ldy) {
-  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (size_t)R * O) return;
-  const int r = (int)(i / O), o = (int)(i % O);
-  float s = b != nullptr ? b[o] : 0.f;
-  for (int k = 0; k < K; ++k) s += x[(size_t)r * ldx + k] * w[(size_t)o * K + k];
-  y[(size_t)r * ldy + o] = s;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < (size_t)R * O; i += (size_t)gridDim.x * 256) {
+    const int r = (int)(i / O), o = (int)(i % O);
+    float s = b != nullptr ? b[o] : 0.f;
+    for (int k = 0; k < K; ++k) s += x[(size_t)r * ldx + k] * w[(size_t)o * K + k];
+    y[(size_t)r * ldy + o] = s;
+  }
 }
 static __global__ void silu_fwd_kernel(const float* x, float* y, size_t n) {
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) y[i] = silu(x[i]);

@@ -84,8 +84,12 @@ static void run_arena(dmx_model* m, hipStream_t st, Arena& A, void*& mem, size_t
   A.base = nullptr;
   A.off = 0;
   A.plan = true;
+  std::vector<size_t> trace;
+  A.trace = check_args() ? &trace : nullptr;
+  A.n = 0;
   {
     Run R{m, st, true, A};
+    A.layer = &R.layer;
     body(R);
   }
   if (A.off > cap) {
@@ -98,11 +102,24 @@ static void run_arena(dmx_model* m, hipStream_t st, Arena& A, void*& mem, size_t
     HIPCHK(hipMalloc(&mem, A.off));
     cap = A.off;
   }
+  const size_t planned = A.off;
+  poison(mem, A.off, st);
   A.base = static_cast<char*>(mem);
   A.off = 0;
   A.plan = false;
+  A.n = 0;
   Run R{m, st, false, A};
-  body(R);
+  A.layer = &R.layer;
+  try {
+    body(R);
+  } catch (...) {
+    A.trace = nullptr;
+    A.layer = nullptr;
+    throw;
+  }
+  A.trace = nullptr;
+  A.layer = nullptr;
+  if (A.off != planned) throw Error(DMX_E_INTERNAL, "workspace plan / run mismatch");
 }
 
 // ---------------------------------------------------------------------------
@@ -450,6 +467,8 @@ static void wgrad(Run& R, const float* dy, const float* x, int N, int H, int W, 
   splits = cdiv(M, rps);
   float* part = R.ws.get<float>((size_t)splits * Cout * K);
   if (R.plan) return;
+  check_range(R, dy, (size_t)M * Cout * 4, "wgrad dY");
+  check_range(R, x, (size_t)M * Cin * 4, "wgrad X");
   WgradParams p{dy, x, N, H, W, Cin, Cout, taps, M, K, rps, part};
   R.begin("wgrad_kernel", 2.0 * M * (double)Cout * K, 4.0 * ((double)M * (Cout + Cin) + (double)splits * Cout * K));
   wgrad_kernel<<<dim3(cdiv(Cout, 64), cdiv(K, 64), splits), 256, 0, R.st>>>(p);

@@ -1,0 +1,83 @@
+"""No kernel reads workspace it did not write: the same inference step (CFG, B = 5 and its 3 + 2
+shards) and training forward / backward run in two fresh processes, one with every workspace
+filled with 0xFF bytes (fp32 NaN) before use (DMX_POISON=1, engine.hip poison()), one without.
+Outputs must be finite and bit-identical: a read of stale memory would turn them NaN (or make
+results depend on what a previous model left in reused device memory)."""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+WORKER = r'''
+import os, sys
+import torch
+import torch.nn.functional as F
+sys.path[:0] = [os.path.join(ROOT, "diffusion-model_amd"), ROOT, os.path.join(ROOT, "tests")]
+import diff
+from dmx import synth
+from models.unet_cond_geom import UnetCondWithGeomHead
+dev = torch.device("cuda:0")
+m = UnetCondWithGeomHead()
+m.load_state_dict(synth.unet_cond_geom_weights(0))
+m.to(dev).eval()
+d = diff.Diffuser(4, device=dev)
+tables = d.coef_tables(dev, clamp_prev=True)
+nm = m.native()
+g = torch.Generator().manual_seed(40)
+B = 5
+vals = torch.rand((B, 12), generator=g).to(dev)
+mask = (torch.rand((B, 12), generator=g) > 0.3).float().to(dev)
+y = torch.tensor([1] * 3 + [3] * (B - 3), device=dev)
+out = {}
+for hw in (16, 28):
+    x = torch.randn((B, 4, hw, hw), generator=g).to(dev)
+    noise = torch.randn((B, 4, hw, hw), generator=g).to(dev)
+    for prec in ("x3", "fp32"):
+        with nm.precision_override(prec):
+            tt = torch.full((B,), 4, dtype=torch.long, device=dev)
+            for s, e in ((0, B), (0, 3), (3, B)):
+                o = torch.empty_like(x[s:e])
+                nm.step(x[s:e].contiguous(), o, tt[s:e], y[s:e], 0, vals[s:e].contiguous(), mask[s:e].contiguous(),
+                        3.0, tables, noise[s:e].contiguous())
+                out[f"step{hw}_{prec}_{s}_{e}"] = o.cpu()
+m.train()
+x = torch.randn((2, 4, 28, 28), generator=g).to(dev)
+t = torch.tensor([17, 900], device=dev)
+eps, geom, tape = nm.train_forward(x, t, y[:2], vals[:2], mask[:2])
+grads = nm.train_backward(tape, torch.randn(eps.shape, generator=g).to(dev), torch.randn(geom.shape, generator=g).to(dev))
+out["train_eps"], out["train_geom"] = eps.cpu(), geom.cpu()
+for k, v in grads.items():
+    out["grad_" + k] = v.cpu()
+torch.cuda.synchronize()
+torch.save(out, sys.argv[1])
+print("[poison-worker] ok", flush=True)
+'''
+
+
+def _run(tmp_path, poison):
+    path = str(tmp_path / f"out_{poison}.pt")
+    env = dict(os.environ, DMX_POISON=str(poison))
+    r = subprocess.run([sys.executable, "-c", f"ROOT = {ROOT!r}\n" + WORKER, path], env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    return torch.load(path, weights_only=True)
+
+
+def test_no_reads_of_unwritten_workspace(cuda, tmp_path):
+    clean = _run(tmp_path, 0)
+    poisoned = _run(tmp_path, 1)
+    bad = [k for k in clean if not torch.isfinite(poisoned[k]).all() or not torch.equal(clean[k], poisoned[k])]
+    assert bad == [], bad[:10]
+    # shard consistency (same process, same kernels): B = 5 equals its 3 + 2 shards
+    for hw in (16, 28):
+        for prec in ("x3", "fp32"):
+            full = clean[f"step{hw}_{prec}_0_5"]
+            parts = torch.cat([clean[f"step{hw}_{prec}_0_3"], clean[f"step{hw}_{prec}_3_5"]])
+            assert torch.equal(full, parts), (hw, prec, float((full - parts).abs().max()))
