@@ -39,9 +39,12 @@ struct GnBwdParams {
   float* dr;             // [N][HW][C]
   float* dres;           // residual gradient dy (res != null): dres_mode 1 writes, 2 accumulates
   int dres_mode;
-  float* sums;           // [N][2]: S1, S2 (pass A out)
-  float* chpart;         // [N][2][C]: per-sample dgamma, dbeta partials (pass A out)
+  float* sums;           // [N][2]: S1, S2 (finish out)
+  float* chpart;         // [N][2][C]: per-sample dgamma, dbeta sums (finish out)
   float* demb; int demb_stride, demb_off;  // or null: demb[n][off + c] = sum over pixels of dout
+  int chunks, ppb;       // pass A: blocks per sample, pixels per block
+  double* bsum;          // [N][chunks][2] block partials of S1, S2
+  float* bch;            // [N][chunks][3][C] block partials of dgamma, dbeta, demb
 };
 
 DMX_DEV float2 gn_stats_from_rowpart(const GnBwdParams& p, int n, double* red) {
@@ -86,21 +89,24 @@ DMX_DEV float gn_dy(const GnBwdParams& p, size_t idx, int c, float xh, float& dr
   return d;
 }
 
-// Thread -> (channels, pixels) ownership: C >= 256: channels tid + 256 q (q < C / 256), every
-// pixel; C < 256 (C | 256): channel tid % C, pixels tid / C + k (256 / C).  Coalesced rows.
+// Pass A, grid (chunks, N): block b of sample n takes pixels [b ppb, (b + 1) ppb).  Thread ->
+// (channels, pixels) ownership: C >= 256: channels tid + 256 q (q < C / 256), every pixel;
+// C < 256 (C | 256): channel tid % C, pixels tid / C + k (256 / C).  Coalesced rows.  Block
+// partials are combined in a fixed order by gn_bwd_finish_kernel.
 static __global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const GnBwdParams p) {
   __shared__ double red[8];
   __shared__ float tg[3][2][256];
   __shared__ double sr[8];
-  const int n = blockIdx.x, tid = threadIdx.x;
+  const int n = blockIdx.y, b = blockIdx.x, tid = threadIdx.x;
   const float2 st = gn_stats_from_rowpart(p, n, red);
   const bool wide = p.C >= 256;
   const int cpt = wide ? p.C / 256 : 1, pstep = wide ? 1 : 256 / p.C;
   const int c0 = wide ? tid : tid % p.C, p0 = wide ? 0 : tid / p.C;
   const size_t base = (size_t)n * p.HW * p.C;
+  const int pbeg = b * p.ppb, pend = min(p.HW, pbeg + p.ppb);
   float s1 = 0.f, s2 = 0.f;
   float g1[2] = {0.f, 0.f}, b1[2] = {0.f, 0.f}, e1[2] = {0.f, 0.f};
-  for (int pix = p0; pix < p.HW; pix += pstep) {
+  for (int pix = pbeg + p0; pix < pend; pix += pstep) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       if (q >= cpt) break;
@@ -134,9 +140,10 @@ static __global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const GnBwdPa
     sr[4 + (tid >> 6)] = d2;
   }
   __syncthreads();
+  const size_t blk = (size_t)n * p.chunks + b;
   if (tid == 0) {
-    p.sums[2 * n] = (float)((sr[0] + sr[1]) + (sr[2] + sr[3]));
-    p.sums[2 * n + 1] = (float)((sr[4] + sr[5]) + (sr[6] + sr[7]));
+    p.bsum[2 * blk] = (sr[0] + sr[1]) + (sr[2] + sr[3]);
+    p.bsum[2 * blk + 1] = (sr[4] + sr[5]) + (sr[6] + sr[7]);
   }
   // per-channel sums over the threads sharing a channel, in thread order (deterministic)
   for (int c = tid; c < p.C; c += 256) {
@@ -152,6 +159,33 @@ static __global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const GnBwdPa
         a1 += tg[1][0][t];
         a2 += tg[2][0][t];
       }
+    }
+    float* o = p.bch + blk * 3 * p.C;
+    o[c] = a0;
+    o[p.C + c] = a1;
+    o[2 * p.C + c] = a2;
+  }
+}
+
+// Block partials -> per-sample S1, S2, dgamma / dbeta rows and the emb gradient (chunk order).
+static __global__ __launch_bounds__(256) void gn_bwd_finish_kernel(const GnBwdParams p) {
+  const int n = blockIdx.x, tid = threadIdx.x;
+  if (tid == 0) {
+    double a = 0.0, b = 0.0;
+    for (int k = 0; k < p.chunks; ++k) {
+      a += p.bsum[2 * ((size_t)n * p.chunks + k)];
+      b += p.bsum[2 * ((size_t)n * p.chunks + k) + 1];
+    }
+    p.sums[2 * n] = (float)a;
+    p.sums[2 * n + 1] = (float)b;
+  }
+  for (int c = tid; c < p.C; c += 256) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    for (int k = 0; k < p.chunks; ++k) {
+      const float* o = p.bch + ((size_t)n * p.chunks + k) * 3 * p.C;
+      a0 += o[c];
+      a1 += o[p.C + c];
+      a2 += o[2 * p.C + c];
     }
     p.chpart[((size_t)n * 2 + 0) * p.C + c] = a0;
     p.chpart[((size_t)n * 2 + 1) * p.C + c] = a1;
@@ -179,13 +213,31 @@ static __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const GnBwdPar
   }
 }
 
-// Column sums of [R][C] partial rows in row order (fixed): out[c] (+)= sum_r in[r * stride + c].
-static __global__ void colsum_kernel(const float* in, int R, int C, size_t stride, float* out, int accumulate) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
-  float s = 0.f;
-  for (int r = 0; r < R; ++r) s += in[(size_t)r * stride + c];
-  out[c] = accumulate ? out[c] + s : s;
+// Column sums: out[y][c] (+)= sum over rows [y rpb, min(R, (y + 1) rpb)) of in[r * stride + c];
+// grid (cdiv(C, 64), row blocks), 4 row groups x 64 columns per block, combined in a fixed order.
+static __global__ __launch_bounds__(256) void colsum_kernel(const float* in, int R, int C, size_t stride, int rpb,
+                                                          float* out, int accumulate) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
+  const int r0 = blockIdx.y * rpb, r1 = min(R, r0 + rpb);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;  // 4 independent chains keep loads in flight
+  if (c < C) {
+    int r = r0 + rg;
+    for (; r + 12 < r1; r += 16) {
+      s0 += in[(size_t)r * stride + c];
+      s1 += in[(size_t)(r + 4) * stride + c];
+      s2 += in[(size_t)(r + 8) * stride + c];
+      s3 += in[(size_t)(r + 12) * stride + c];
+    }
+    for (; r < r1; r += 4) s0 += in[(size_t)r * stride + c];
+  }
+  red[rg][cl] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (rg == 0 && c < C) {
+    const float v = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+    float* o = out + (size_t)blockIdx.y * C + c;
+    *o = accumulate ? *o + v : v;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -199,37 +251,38 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* x, const float
   constexpr int C = CPL * 64;
   __shared__ float pg[4][C], pb[4][C];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + wv;
-  float v[CPL], g[CPL];
-  const bool ok = row < M;
-  float s = 0.f;
+  float ag[CPL], ab[CPL];  // this lane's dgamma / dbeta partials over the wave's rows
 #pragma unroll
-  for (int j = 0; j < CPL; ++j) {
-    v[j] = ok ? x[(size_t)row * C + lane + 64 * j] : 0.f;
-    s += v[j];
-  }
-  const float mean = wave_sum(s) / (float)C;
-  float q = 0.f;
+  for (int j = 0; j < CPL; ++j) ag[j] = ab[j] = 0.f;
+  for (int row = blockIdx.x * 4 + wv; row < M; row += gridDim.x * 4) {
+    float v[CPL], g[CPL];
+    float s = 0.f;
 #pragma unroll
-  for (int j = 0; j < CPL; ++j) {
-    const float d = v[j] - mean;
-    q += d * d;
-  }
-  const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)C + 1e-5f);
-  float a1 = 0.f, a2 = 0.f;
+    for (int j = 0; j < CPL; ++j) {
+      v[j] = x[(size_t)row * C + lane + 64 * j];
+      s += v[j];
+    }
+    const float mean = wave_sum(s) / (float)C;
+    float q = 0.f;
 #pragma unroll
-  for (int j = 0; j < CPL; ++j) {
-    const int c = lane + 64 * j;
-    const float xh = (v[j] - mean) * rstd;
-    g[j] = ok ? dy[(size_t)row * C + c] : 0.f;
-    const float gd = g[j] * w[c];
-    a1 += gd;
-    a2 += gd * xh;
-    pg[wv][c] = g[j] * xh;
-    pb[wv][c] = g[j];
-  }
-  const float m1 = wave_sum(a1) / (float)C, m2 = wave_sum(a2) / (float)C;
-  if (ok) {
+    for (int j = 0; j < CPL; ++j) {
+      const float d = v[j] - mean;
+      q += d * d;
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)C + 1e-5f);
+    float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) {
+      const int c = lane + 64 * j;
+      const float xh = (v[j] - mean) * rstd;
+      g[j] = dy[(size_t)row * C + c];
+      const float gd = g[j] * w[c];
+      a1 += gd;
+      a2 += gd * xh;
+      ag[j] += g[j] * xh;
+      ab[j] += g[j];
+    }
+    const float m1 = wave_sum(a1) / (float)C, m2 = wave_sum(a2) / (float)C;
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {
       const int c = lane + 64 * j;
@@ -238,6 +291,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* x, const float
       float* o = dx + (size_t)row * C + c;
       *o = accumulate ? *o + r : r;
     }
+  }
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) {
+    pg[wv][lane + 64 * j] = ag[j];
+    pb[wv][lane + 64 * j] = ab[j];
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += 256) {
@@ -260,6 +318,7 @@ struct WgradParams {
   int M, K;          // M = N*H*W rows, K = taps * Cin
   int rows_per_split;
   float* part;       // [splits][Cout][K]
+  float* bpart;      // wgrad_fast_kernel: [splits][Cout] column sums of dY (bias gradient), or null
 };
 
 static __global__ __launch_bounds__(256) void wgrad_kernel(const WgradParams p) {
@@ -308,6 +367,97 @@ static __global__ __launch_bounds__(256) void wgrad_kernel(const WgradParams p) 
     const int k = k0 + wn * 32 + (lane & 31);
     if (co < p.Cout && k < p.K) dst[(size_t)co * p.K + k] = acc[r];
   }
+}
+
+// Fast path (Cin % 64 == 0, Cout % 64 == 0): block tile 64 (co) x 128 (k), the rows streamed in
+// stages of 32 through double-buffered LDS with float4 global loads issued one stage ahead
+// (register prefetch), 4 waves 2 x 2 each owning 32 co x 64 k (two 32x32 accumulators).
+// A 64-wide k slice lies inside one tap (Cin % 64 == 0), so a thread's tap / channel offset is
+// fixed and only its rows' (n, y, x) are decoded per stage.
+constexpr int WG_BM = 32;
+static __global__ __launch_bounds__(256) void wgrad_fast_kernel(const WgradParams p) {
+  __shared__ __attribute__((aligned(16))) float dys[2][WG_BM][64 + 4];
+  __shared__ __attribute__((aligned(16))) float xs[2][WG_BM][128 + 4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv >> 1, wn = wv & 1;
+  const int co0 = blockIdx.x * 64, k0 = blockIdx.y * 128;
+  const int mbeg = blockIdx.z * p.rows_per_split, mend = min(p.M, mbeg + p.rows_per_split);
+  const int HW = p.H * p.W;
+  // dY: 32 rows x 16 float4 -> thread (row tid / 16 + 16 i, float4 tid % 16), i < 2
+  const int dr = tid >> 4, dc = (tid & 15) * 4;
+  // X: 32 rows x 32 float4 -> thread (row tid / 32 + 8 i, float4 tid % 32), i < 4
+  const int xr = tid >> 5, xc = (tid & 31) * 4;
+  const int k = k0 + xc;
+  const bool kvalid = k < p.K;
+  const int tap = kvalid ? k / p.Cin : 0, ci = k - tap * p.Cin;
+  const int ty = p.taps == 9 ? tap / 3 - 1 : 0, tx = p.taps == 9 ? tap % 3 - 1 : 0;
+  floatx4 rd[2], rx[4];
+  auto load = [&](int m0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = m0 + dr + 16 * i;
+      rd[i] = m < mend ? *reinterpret_cast<const floatx4*>(p.dy + (size_t)m * p.Cout + co0 + dc)
+                       : floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + xr + 8 * i;
+      floatx4 v = {0.f, 0.f, 0.f, 0.f};
+      if (m < mend && kvalid) {
+        const int n = m / HW, rr = m - n * HW, y = rr / p.W, xx = rr - y * p.W;
+        const int iy = y + ty, ix = xx + tx;
+        if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W)
+          v = *reinterpret_cast<const floatx4*>(p.x + (((size_t)n * p.H + iy) * p.W + ix) * p.Cin + ci);
+      }
+      rx[i] = v;
+    }
+  };
+  auto store = [&](int b) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) *reinterpret_cast<floatx4*>(&dys[b][dr + 16 * i][dc]) = rd[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<floatx4*>(&xs[b][xr + 8 * i][xc]) = rx[i];
+  };
+  floatx16 acc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  const bool bias = p.bpart != nullptr && blockIdx.y == 0;
+  float bsum = 0.f;  // threads 0..63 of a k-tile-0 block: column sum of dY over this split's rows
+  const int nst = (mend - mbeg + WG_BM - 1) / WG_BM;
+  if (nst > 0) {
+    load(mbeg);
+    store(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const int b = st & 1;
+    if (st + 1 < nst) load(mbeg + (st + 1) * WG_BM);
+#pragma unroll
+    for (int s = 0; s < WG_BM; s += 2) {
+      const float a = dys[b][s + (lane >> 5)][wm * 32 + (lane & 31)];
+      const float b0 = xs[b][s + (lane >> 5)][wn * 64 + (lane & 31)];
+      const float b1 = xs[b][s + (lane >> 5)][wn * 64 + 32 + (lane & 31)];
+      acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b0, acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b1, acc[1], 0, 0, 0);
+    }
+    if (bias && tid < 64) {
+#pragma unroll 8
+      for (int s = 0; s < WG_BM; ++s) bsum += dys[b][s][tid];
+    }
+    if (st + 1 < nst) store(b ^ 1);
+    __syncthreads();
+  }
+  if (bias && tid < 64) p.bpart[(size_t)blockIdx.z * p.Cout + co0 + tid] = bsum;
+  float* dst = p.part + (size_t)blockIdx.z * p.Cout * p.K;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = co0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      const int kk = k0 + wn * 64 + j * 32 + (lane & 31);
+      if (kk < p.K) dst[(size_t)co * p.K + kk] = acc[j][r];
+    }
 }
 
 // grad (torch layout) = sum over splits (split order); k = tap * Cin + ci -> [co][ci][tap]
@@ -661,17 +811,6 @@ static __global__ void gap_bwd_kernel(const float* dg, int N, int HW, float* dfe
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
     const int k = (int)(i % 64), n = (int)(i / ((size_t)HW * 64));
     dfeat[i] += dg[n * 64 + k] / (float)HW;
-  }
-}
-
-// Per-channel sum of dY [M][C] (bias gradients of Linear layers / conv biases): part[blocks][C].
-static __global__ __launch_bounds__(256) void rowsum_part_kernel(const float* dy, int M, int C, int rows_per_block,
-                                                                 float* part) {
-  const int r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float s = 0.f;
-    for (int r = r0; r < r1; ++r) s += dy[(size_t)r * C + c];
-    part[(size_t)blockIdx.x * C + c] = s;
   }
 }
 

@@ -441,41 +441,53 @@ static void train_fwd_body(Run& R, Tape& T, const TrainArgs& a) {
 // ---------------------------------------------------------------------------
 // backward building blocks
 // ---------------------------------------------------------------------------
+// out[c] = sum over `rows` rows of in[r * stride + c]: one pass for <= 256 rows, else row
+// blocks of 256 into a partial table, then that table's column sums (fixed order).
 static void colsum(Run& R, const float* in, int rows, int C, size_t stride, float* out) {
+  const int rpb = 256, nb = cdiv(rows, rpb);
+  float* part = nb > 1 ? R.ws.get<float>((size_t)nb * C) : nullptr;
   if (R.plan) return;
-  colsum_kernel<<<cdiv(C, 256), 256, 0, R.st>>>(in, rows, C, stride, out, 0);
+  if (nb == 1) {
+    colsum_kernel<<<dim3(cdiv(C, 64), 1), 256, 0, R.st>>>(in, rows, C, stride, rows, out, 0);
+  } else {
+    colsum_kernel<<<dim3(cdiv(C, 64), nb), 256, 0, R.st>>>(in, rows, C, stride, rpb, part, 0);
+    colsum_kernel<<<dim3(cdiv(C, 64), 1), 256, 0, R.st>>>(part, nb, C, C, nb, out, 0);
+  }
   HIPCHK(hipGetLastError());
 }
 
-// bias gradient = column sums of dY [M][C] (fixed order: 256-row blocks, then blocks in order)
-static void bias_grad(Run& R, const float* dy, int M, int C, float* out) {
-  const int rpb = 256, nb = cdiv(M, rpb);
-  float* part = R.ws.get<float>((size_t)nb * C);
-  if (R.plan) return;
-  rowsum_part_kernel<<<nb, 256, 0, R.st>>>(dy, M, C, rpb, part);
-  HIPCHK(hipGetLastError());
-  colsum(R, part, nb, C, C, out);
-}
+// bias gradient = column sums of dY [M][C]
+static void bias_grad(Run& R, const float* dy, int M, int C, float* out) { colsum(R, dy, M, C, C, out); }
 
 // weight gradient of a conv3x3 (taps 9) / Linear (taps 1) over NHWC input x and NHWC dY
 static void wgrad(Run& R, const float* dy, const float* x, int N, int H, int W, int Cin, int Cout, int taps,
-                  int cin_real, float* grad) {
+                  int cin_real, float* grad, float* bias_grad_out = nullptr) {
   const int M = N * H * W, K = taps * Cin;
-  const int bxy = cdiv(Cout, 64) * cdiv(K, 64);
+  const bool fast = Cin % 64 == 0 && Cout % 64 == 0;
+  const int bxy = cdiv(Cout, 64) * cdiv(K, fast ? 128 : 64);
   int splits = std::max(1, std::min(cdiv(1024, bxy), cdiv(M, 256)));
   const int rps = rup(cdiv(M, splits), 16);
   splits = cdiv(M, rps);
   float* part = R.ws.get<float>((size_t)splits * Cout * K);
-  if (R.plan) return;
-  check_range(R, dy, (size_t)M * Cout * 4, "wgrad dY");
-  check_range(R, x, (size_t)M * Cin * 4, "wgrad X");
-  WgradParams p{dy, x, N, H, W, Cin, Cout, taps, M, K, rps, part};
-  R.begin("wgrad_kernel", 2.0 * M * (double)Cout * K, 4.0 * ((double)M * (Cout + Cin) + (double)splits * Cout * K));
-  wgrad_kernel<<<dim3(cdiv(Cout, 64), cdiv(K, 64), splits), 256, 0, R.st>>>(p);
-  R.end();
-  HIPCHK(hipGetLastError());
-  wgrad_finish_kernel<<<ew_blocks((size_t)Cout * K), 256, 0, R.st>>>(part, splits, Cout, Cin, cin_real, taps, grad);
-  HIPCHK(hipGetLastError());
+  // bias gradient: column sums of dY, from the fast kernel's k-tile-0 blocks (per split)
+  float* bpart = (bias_grad_out != nullptr && fast) ? R.ws.get<float>((size_t)splits * Cout) : nullptr;
+  if (!R.plan) {
+    check_range(R, dy, (size_t)M * Cout * 4, "wgrad dY");
+    check_range(R, x, (size_t)M * Cin * 4, "wgrad X");
+    WgradParams p{dy, x, N, H, W, Cin, Cout, taps, M, K, rps, part, bpart};
+    R.begin("wgrad_kernel", 2.0 * M * (double)Cout * K, 4.0 * ((double)M * (Cout + Cin) + (double)splits * Cout * K));
+    if (fast) wgrad_fast_kernel<<<dim3(Cout / 64, cdiv(K, 128), splits), 256, 0, R.st>>>(p);
+    else wgrad_kernel<<<dim3(cdiv(Cout, 64), cdiv(K, 64), splits), 256, 0, R.st>>>(p);
+    R.end();
+    HIPCHK(hipGetLastError());
+    wgrad_finish_kernel<<<ew_blocks((size_t)Cout * K), 256, 0, R.st>>>(part, splits, Cout, Cin, cin_real, taps, grad);
+    HIPCHK(hipGetLastError());
+  }
+  // bias gradient = column sums of dY: the fast kernel's per-split sums, else a pass over dY
+  if (bias_grad_out != nullptr) {
+    if (fast) colsum(R, bpart, splits, Cout, Cout, bias_grad_out);
+    else bias_grad(R, dy, M, Cout, bias_grad_out);
+  }
 }
 
 // data gradient through a packed transposed / flipped weight: dx (+)= dY * W'
@@ -484,12 +496,31 @@ static void dgrad(Run& R, const float* dy, int Cy, int N, int H, int W, const Co
        accumulate ? dx : nullptr, nullptr, 1);
 }
 
+static void gn_bwd_launch(Run& R, const float* r, const float2* rp, int nseg, int rrows, const Vec& g, const Vec& b,
+                          const float* res, int act, const float* dout, int N, int C, int HW, float* dr, float* dres,
+                          int dres_mode, float* sums, float* chpart, float* demb, int demb_stride, int demb_off,
+                          int ppb, double* bsum, float* bch);
+
 static void gn_bwd(Run& R, const float* r, const float2* rp, int nseg, int rrows, const Vec& g, const Vec& b,
                    const float* res, int act, const float* dout, int N, int C, int HW, float* dr, float* dres,
                    int dres_mode, float* ggamma, float* gbeta, float* demb, int demb_stride, int demb_off) {
+  // pass A over ~512 blocks in total (>= 16 pixels each)
+  const int chunks = std::max(1, std::min(cdiv(512, N), cdiv(HW, 16)));
+  const int ppb = cdiv(HW, chunks);
   float* sums = R.ws.get<float>((size_t)2 * N);
   float* chpart = R.ws.get<float>((size_t)N * 2 * C);
-  if (R.plan) return;
+  double* bsum = R.ws.get<double>((size_t)N * chunks * 2);
+  float* bch = R.ws.get<float>((size_t)N * chunks * 3 * C);
+  if (!R.plan) gn_bwd_launch(R, r, rp, nseg, rrows, g, b, res, act, dout, N, C, HW, dr, dres, dres_mode, sums, chpart,
+                             demb, demb_stride, demb_off, ppb, bsum, bch);
+  colsum(R, chpart, N, C, 2 * (size_t)C, ggamma);
+  colsum(R, chpart + C, N, C, 2 * (size_t)C, gbeta);
+}
+
+static void gn_bwd_launch(Run& R, const float* r, const float2* rp, int nseg, int rrows, const Vec& g, const Vec& b,
+                          const float* res, int act, const float* dout, int N, int C, int HW, float* dr, float* dres,
+                          int dres_mode, float* sums, float* chpart, float* demb, int demb_stride, int demb_off,
+                          int ppb, double* bsum, float* bch) {
   GnBwdParams p;
   std::memset(&p, 0, sizeof(p));
   p.r = r;
@@ -511,33 +542,37 @@ static void gn_bwd(Run& R, const float* r, const float2* rp, int nseg, int rrows
   p.demb = demb;
   p.demb_stride = demb_stride;
   p.demb_off = demb_off;
+  p.chunks = cdiv(HW, ppb);
+  p.ppb = ppb;
+  p.bsum = bsum;
+  p.bch = bch;
   R.begin("gn_bwd_reduce_kernel", 0.0, 4.0 * (double)N * HW * C * (res ? 3 : 2));
-  gn_bwd_reduce_kernel<<<N, 256, 0, R.st>>>(p);
+  gn_bwd_reduce_kernel<<<dim3(p.chunks, N), 256, 0, R.st>>>(p);
+  gn_bwd_finish_kernel<<<N, 256, 0, R.st>>>(p);
   R.end();
   HIPCHK(hipGetLastError());
-  const int chunks = std::max(1, std::min(64, cdiv(HW * C, 4096)));
+  const int achunks = std::max(1, std::min(64, cdiv(HW * C, 4096)));
   R.begin("gn_bwd_apply_kernel", 0.0, 4.0 * (double)N * HW * C * (res ? 4 : 3));
-  gn_bwd_apply_kernel<<<dim3(chunks, N), 256, 0, R.st>>>(p);
+  gn_bwd_apply_kernel<<<dim3(achunks, N), 256, 0, R.st>>>(p);
   R.end();
   HIPCHK(hipGetLastError());
-  colsum(R, chpart, N, C, 2 * (size_t)C, ggamma);
-  colsum(R, chpart + C, N, C, 2 * (size_t)C, gbeta);
 }
 
 static void ln_bwd(Run& R, const float* x, const Vec& w, const float* dy, float* dx, bool accumulate, int M, int C,
                    float* gw, float* gb) {
-  const int blocks = cdiv(M, 4);
+  const int blocks = std::min(cdiv(M, 4), 512);
   float* part = R.ws.get<float>((size_t)blocks * 2 * C);
-  if (R.plan) return;
-  R.begin("ln_bwd_kernel", 0.0, 4.0 * (double)M * C * 3);
-  switch (C) {
-    case 64: ln_bwd_kernel<1><<<blocks, 256, 0, R.st>>>(x, w.p, dy, dx, accumulate ? 1 : 0, part, M); break;
-    case 128: ln_bwd_kernel<2><<<blocks, 256, 0, R.st>>>(x, w.p, dy, dx, accumulate ? 1 : 0, part, M); break;
-    case 256: ln_bwd_kernel<4><<<blocks, 256, 0, R.st>>>(x, w.p, dy, dx, accumulate ? 1 : 0, part, M); break;
-    default: throw Error(DMX_E_INTERNAL, "ln_bwd: unsupported C");
+  if (!R.plan) {
+    R.begin("ln_bwd_kernel", 0.0, 4.0 * (double)M * C * 3);
+    switch (C) {
+      case 64: ln_bwd_kernel<1><<<blocks, 256, 0, R.st>>>(x, w.p, dy, dx, accumulate ? 1 : 0, part, M); break;
+      case 128: ln_bwd_kernel<2><<<blocks, 256, 0, R.st>>>(x, w.p, dy, dx, accumulate ? 1 : 0, part, M); break;
+      case 256: ln_bwd_kernel<4><<<blocks, 256, 0, R.st>>>(x, w.p, dy, dx, accumulate ? 1 : 0, part, M); break;
+      default: throw Error(DMX_E_INTERNAL, "ln_bwd: unsupported C");
+    }
+    R.end();
+    HIPCHK(hipGetLastError());
   }
-  R.end();
-  HIPCHK(hipGetLastError());
   colsum(R, part, blocks, C, 2 * (size_t)C, gw);
   colsum(R, part + C, blocks, C, 2 * (size_t)C, gb);
 }
@@ -595,30 +630,26 @@ static void attn_bwd(Run& R, const TAttn& t, const GradMap& G, float* dout, floa
   const int C = a.c, N = t.N, H = t.H, W = t.W, M = N * H * W, L = H * W;
   const std::string& p = a.prefix;
   // out = ff2(gelu(ff1(al))) + av
-  wgrad(R, dout, t.f, N, H, W, C, C, 1, C, G(p + ".ff_self.3.weight"));
-  bias_grad(R, dout, M, C, G(p + ".ff_self.3.bias"));
+  wgrad(R, dout, t.f, N, H, W, C, C, 1, C, G(p + ".ff_self.3.weight"), G(p + ".ff_self.3.bias"));
   float* dh = R.ws.get<float>((size_t)M * C);
   dgrad(R, dout, C, N, H, W, a.df2, dh, false);
   if (!R.plan) {
     gelu_bwd_kernel<<<ew_blocks((size_t)M * C), 256, 0, R.st>>>(dh, t.h1, dh, (size_t)M * C);
     HIPCHK(hipGetLastError());
   }
-  wgrad(R, dh, t.al, N, H, W, C, C, 1, C, G(p + ".ff_self.1.weight"));
-  bias_grad(R, dh, M, C, G(p + ".ff_self.1.bias"));
+  wgrad(R, dh, t.al, N, H, W, C, C, 1, C, G(p + ".ff_self.1.weight"), G(p + ".ff_self.1.bias"));
   float* dal = R.ws.get<float>((size_t)M * C);
   dgrad(R, dh, C, N, H, W, a.df1, dal, false);
   // al = LN2(av): dav = dout + LN2^T(dal)
   ln_bwd(R, t.av, a.l2w, dal, dout, true, M, C, G(p + ".ff_self.0.weight"), G(p + ".ff_self.0.bias"));
   float* dav = dout;
   // av = out_proj(attn(xl)) + xl
-  wgrad(R, dav, t.ao, N, H, W, C, C, 1, C, G(p + ".mha.out_proj.weight"));
-  bias_grad(R, dav, M, C, G(p + ".mha.out_proj.bias"));
+  wgrad(R, dav, t.ao, N, H, W, C, C, 1, C, G(p + ".mha.out_proj.weight"), G(p + ".mha.out_proj.bias"));
   float* dao = R.ws.get<float>((size_t)M * C);
   dgrad(R, dav, C, N, H, W, a.dout, dao, false);
   float* dqkv = R.ws.get<float>((size_t)M * 3 * C);
   attn_core_bwd(R, t.qkv, t.ao, dao, dqkv, N, L, C);
-  wgrad(R, dqkv, t.xl, N, H, W, C, 3 * C, 1, C, G(p + ".mha.in_proj_weight"));
-  bias_grad(R, dqkv, M, 3 * C, G(p + ".mha.in_proj_bias"));
+  wgrad(R, dqkv, t.xl, N, H, W, C, 3 * C, 1, C, G(p + ".mha.in_proj_weight"), G(p + ".mha.in_proj_bias"));
   dgrad(R, dqkv, 3 * C, N, H, W, a.dqkv, dav, true);  // dxl = dav + in_proj^T(dqkv)
   ln_bwd(R, t.x, a.l1w, dav, dx, false, M, C, G(p + ".ln.weight"), G(p + ".ln.bias"));
 }
@@ -661,8 +692,7 @@ static void train_bwd_body(Run& R, Tape& T, const GradMap& G, const float* d_eps
     }
     HIPCHK(hipGetLastError());
   }
-  wgrad(R, dyo, T.feat, N, H, W, 64, Co, 1, 64, G("out.weight"));
-  bias_grad(R, dyo, M, Co, G("out.bias"));
+  wgrad(R, dyo, T.feat, N, H, W, 64, Co, 1, 64, G("out.weight"), G("out.bias"));
   dense_dx(R, dyo, Co, srcp(m, "out.weight"), M, Co, 64, dfeat, 64, false);
   if (m->kind == DMX_UNET_COND_GEOM) {
     const int gh = m->cfg.ghid, gd = m->cfg.gdim;
