@@ -1,23 +1,25 @@
 #!/bin/bash
-# Round evidence for bench.py, written straight into profiles/ (small files only):
-#   profiles/${TAG}_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (graph-replayed steps)
-#   profiles/${TAG}_pmc_traffic.json   FETCH_SIZE / WRITE_SIZE passes -> HBM bytes per launch
-#   profiles/${TAG}_sq_counters.txt    SQ counter passes (MFMA busy, waits, LDS) per kernel
+# Round evidence for bench.py (small files), written to gpurun_out/profiles/ on the GPU box (the
+# directory gpurun copies back); copy them into profiles/ afterwards:
+#   ${TAG}_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (graph-replayed steps)
+#   ${TAG}_pmc_traffic.json   FETCH_SIZE / WRITE_SIZE passes -> HBM bytes per launch
+#   ${TAG}_sq_counters.txt    SQ counter passes (MFMA busy, waits, LDS) per kernel
 # Counter passes never combine --pmc with trace domains (one pass per counter group).
 set -e
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${TAG:-r02}
-mkdir -p gpurun_out profiles
+OUT=gpurun_out/profiles
+mkdir -p $OUT
 ARGS="--steps 10 --warmup 2 --cpu-steps 0 --config4-steps 0 --config5-steps 0 --legs-steps 0 --png-steps 0 --train-steps 0"
 PMC_ARGS="$ARGS --no-profile"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/prof_trace.log 2>&1
-cp "$(find gpurun_out/prof_trace -name '*kernel_stats.csv' | head -1)" profiles/${TAG}_kernel_stats.csv
+cp "$(find gpurun_out/prof_trace -name '*kernel_stats.csv' | head -1)" $OUT/${TAG}_kernel_stats.csv
 rm -f gpurun_out/prof_trace/*kernel_trace.csv
 echo "[profile] trace ok"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch -o run --output-format csv -- python3 bench.py $PMC_ARGS > gpurun_out/prof_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write -o run --output-format csv -- python3 bench.py $PMC_ARGS > gpurun_out/prof_write.log 2>&1
-python3 tools/pmc_traffic.py gpurun_out/prof_fetch gpurun_out/prof_write profiles/${TAG}_pmc_traffic.json > gpurun_out/pmc_traffic.txt
+python3 tools/pmc_traffic.py gpurun_out/prof_fetch gpurun_out/prof_write $OUT/${TAG}_pmc_traffic.json > gpurun_out/pmc_traffic.txt
 echo "[profile] traffic ok"
 i=0
 for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES" \
@@ -26,5 +28,5 @@ for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
   timeout -k 10 300 rocprofv3 --pmc $set -d gpurun_out/pmc_sq$i -o run --output-format csv -- python3 bench.py $PMC_ARGS > gpurun_out/pmc_sq$i.log 2>&1
   i=$((i+1))
 done
-python3 tools/pmc_sq.py "igemm|attention|norm|tok_|prep|step_tail|embed" > profiles/${TAG}_sq_counters.txt
+python3 tools/pmc_sq.py "igemm|attention|norm|tok_|prep|step_tail|embed" > $OUT/${TAG}_sq_counters.txt
 echo "[profile] sq ok"
