@@ -1041,6 +1041,16 @@ static void attention_core(Run& R, const float* qkv, float* out, int N, int L, i
   if (R.plan) return;
   const int D = C / 4;
   if (D != 16 && D != 32 && D != 64) throw Error(DMX_E_INTERNAL, "attention: unsupported head dim");
+  if (R.m->prec >= 1 && D == 16 && att16_lds_bytes(L, 0) <= 160 * 1024) {
+    // head resident in LDS (sa5 / sa6): one block per (sample, head), no per-chunk staging
+    const int x1 = R.m->prec == 2 ? 1 : 0, nw = L > 256 ? 16 : 8;
+    R.begin("attention16_kernel<" + std::to_string(nw) + ", " + std::to_string(x1) + ">", 4.0 * N * (double)L * L * C,
+            4.0 * (double)N * L * 4 * C);
+    HIPCHK(launch_attention16(nw, x1, qkv, out, L, C, N, R.st));
+    R.end();
+    HIPCHK(hipGetLastError());
+    return;
+  }
   if (R.m->prec >= 1) {
     dim3 grid(cdiv(L, 128), 4, N);
     const int x1 = R.m->prec == 2 ? 1 : 0, wpe = D == 16 ? 4 : 1;  // D = 16: >= 4 waves / SIMD (register cap)

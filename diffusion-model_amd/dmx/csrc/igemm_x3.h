@@ -539,5 +539,211 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
 }
 
+// ---------------------------------------------------------------------------
+// D = 16 attention core with the whole head resident in LDS (sa5 / sa6: C = 64, L = 256 / 784 /
+// 1024).  Same arithmetic and operation order as attention_x3_kernel<16> (S^T = K Q^T on
+// 32x32x16 MFMAs, log2-domain online softmax over 64-key chunks, O^T += V^T P^T with V^T padded
+// to 32 rows whose row 16 is ones, so the denominator comes off the matrix cores), but one
+// block per (sample, head) stages that head's K and V^T once — f16 hi / lo planes, L x 16 and
+// 16 x L — and then every wave sweeps all keys for its query tiles with no further barrier.
+// The per-chunk staging of the 128-query kernel (two barriers per 64 keys, K / V re-read and
+// re-split by every query block of the head, 2-byte transposed V stores) is gone.
+//
+// LDS (dynamic, Lp = L rounded up to 64): Kh, Kl [Lp][16]; Vh [18][Lp + 8] (rows 0-15 V^T,
+// 16 ones, 17 zeros); Vl [17][Lp + 8] (row 16 zeros).  Lanes 16-31 of a V^T fragment read the
+// constant rows instead of holding padding in LDS.  Keys in [L, Lp) are zero and masked.
+// ---------------------------------------------------------------------------
+__host__ __device__ inline int att16_lp(int L) { return (L + 63) / 64 * 64; }
+__host__ __device__ inline size_t att16_lds_bytes(int L, int x1) {
+  const size_t lp = (size_t)att16_lp(L), vs = lp + 8;
+  return 2 * ((x1 ? 1 : 2) * lp * 16 + (x1 ? 18 : 35) * vs);
+}
+
+template <int NW, int X1 = 0>
+__global__ __launch_bounds__(NW * 64) void attention16_kernel(const float* qkv, float* out, int L, int C) {
+  constexpr int D = 16, KC = 64;
+  extern __shared__ __attribute__((aligned(16))) _Float16 att_lds[];
+  const int Lp = att16_lp(L), VS = Lp + 8;
+  _Float16* Kh = att_lds;
+  _Float16* Kl = Kh + Lp * D;
+  _Float16* Vh = Kl + (X1 ? 0 : Lp * D);
+  _Float16* Vl = Vh + 18 * VS;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int hd = blockIdx.y, n = blockIdx.z;
+  const int fr = lane & 31, fh = lane >> 5;
+  const size_t rs = (size_t)3 * C;
+  const float* base = qkv + (size_t)n * L * rs + hd * D;
+
+  // stage: a unit = 4 consecutive keys x 4 dims (K rows as half4 stores, V^T rows as half4 stores)
+  for (int u = tid; u < Lp; u += NW * 64) {
+    const int k0 = (u >> 2) * 4, d4 = (u & 3) * 4;
+    floatx4 kv[4], vv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool ok = k0 + j < L;
+      const float* r = base + (size_t)(ok ? k0 + j : 0) * rs + d4;
+      kv[j] = ok ? ld4(r + C) : floatx4{0.f, 0.f, 0.f, 0.f};
+      vv[j] = ok ? ld4(r + 2 * C) : floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      half4 h, l;
+      if constexpr (X1) {
+        h = __builtin_convertvector(kv[j], half4);
+      } else {
+        split4(kv[j], h, l);
+        *reinterpret_cast<half4*>(&Kl[(k0 + j) * D + d4]) = l;
+      }
+      *reinterpret_cast<half4*>(&Kh[(k0 + j) * D + d4]) = h;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const floatx4 t = {vv[0][e], vv[1][e], vv[2][e], vv[3][e]};
+      half4 h, l;
+      if constexpr (X1) {
+        h = __builtin_convertvector(t, half4);
+      } else {
+        split4(t, h, l);
+        *reinterpret_cast<half4*>(&Vl[(d4 + e) * VS + k0]) = l;
+      }
+      *reinterpret_cast<half4*>(&Vh[(d4 + e) * VS + k0]) = h;
+    }
+  }
+  for (int i = tid; i < VS; i += NW * 64) {
+    Vh[16 * VS + i] = (_Float16)1.f;
+    Vh[17 * VS + i] = (_Float16)0.f;
+    if constexpr (!X1) Vl[16 * VS + i] = (_Float16)0.f;
+  }
+  __syncthreads();
+
+  const float qscale = 1.4426950408889634f / sqrtf((float)D);
+  const _Float16* vrh = Vh + (fr < 16 ? fr : fr == 16 ? 16 : 17) * VS;  // this lane's V^T row (hi)
+  const _Float16* vrl = Vl + (fr < 16 ? fr : 16) * VS;                  // (lo)
+  const int nqt = (L + 31) / 32;
+  for (int qt = wid; qt < nqt; qt += NW) {
+    const int q = qt * 32 + fr;
+    half8 qh, ql;
+    {
+      floatx4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+      if (q < L) {
+        const float* r = base + (size_t)q * rs + 8 * fh;
+        a = ld4(r);
+        b = ld4(r + 4);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float va = a[j] * qscale, vb = b[j] * qscale;
+        const _Float16 ha = (_Float16)va, hb = (_Float16)vb;
+        qh[j] = ha;
+        ql[j] = (_Float16)(va - (float)ha);
+        qh[j + 4] = hb;
+        ql[j + 4] = (_Float16)(vb - (float)hb);
+      }
+    }
+    floatx16 o;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[r] = 0.f;
+    float mrun = -INFINITY;
+    for (int c0 = 0; c0 < L; c0 += KC) {
+      floatx16 sc[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sc[kt][r] = 0.f;
+        const int krow = (c0 + kt * 32 + fr) * D + 8 * fh;
+        const half8 kh = *reinterpret_cast<const half8*>(&Kh[krow]);
+        if constexpr (!X1) {
+          const half8 kl = *reinterpret_cast<const half8*>(&Kl[krow]);
+          sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kl, qh, sc[kt], 0, 0, 0);
+          sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, ql, sc[kt], 0, 0, 0);
+        }
+        sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, qh, sc[kt], 0, 0, 0);
+      }
+      const int nvalid = L - c0;
+      if (nvalid < KC) {  // ragged last chunk only (uniform branch)
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+            if (key >= nvalid) sc[kt][r] = -INFINITY;
+          }
+      }
+      float mx = sc[0][0];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kt][r]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(mrun, mx);
+      const float alpha = __builtin_amdgcn_exp2f(mrun - mnew);
+      mrun = mnew;
+      // scalar f32 VALU only: packed v_pk_add / v_pk_mul beside MFMAs cost far more issue time
+      // than their two scalar halves (MI355X_MICROARCH.md, constants table)
+      u32x4 phu[2][2], plu[2][2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int jp = 0; jp < 4; ++jp) {
+            f32x2 v;
+            v.x = __builtin_amdgcn_exp2f(sc[kt][8 * s + 2 * jp] - mnew);
+            v.y = __builtin_amdgcn_exp2f(sc[kt][8 * s + 2 * jp + 1] - mnew);
+            unsigned h, l;
+            if constexpr (X1) {
+              h = __builtin_bit_cast(unsigned, __builtin_convertvector(v, half2v));
+              l = 0u;
+            } else {
+              split2(v, h, l);
+            }
+            phu[kt][s][jp] = h;
+            plu[kt][s][jp] = l;
+          }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[r] *= alpha;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const half8 ph = __builtin_bit_cast(half8, phu[kt][s]);
+          const half8 pl = __builtin_bit_cast(half8, plu[kt][s]);
+          const int k0 = c0 + kt * 32 + 16 * s + 4 * fh;
+          half8 vh, vl;
+          const half4 a0 = *reinterpret_cast<const half4*>(vrh + k0);
+          const half4 a1 = *reinterpret_cast<const half4*>(vrh + k0 + 8);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            vh[j] = a0[j];
+            vh[j + 4] = a1[j];
+          }
+          if constexpr (!X1) {
+            const half4 b0 = *reinterpret_cast<const half4*>(vrl + k0);
+            const half4 b1 = *reinterpret_cast<const half4*>(vrl + k0 + 8);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              vl[j] = b0[j];
+              vl[j + 4] = b1[j];
+            }
+            o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph, o, 0, 0, 0);
+            o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, pl, o, 0, 0, 0);
+          }
+          o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, o, 0, 0, 0);
+        }
+    }
+    const float inv = 1.0f / __shfl(o[8], fr, 64);  // O^T row 16 (the ones row) = the denominator
+    if (q < L) {
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const int d = 8 * g + 4 * fh;
+        floatx4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = o[4 * g + j] * inv;
+        *reinterpret_cast<floatx4*>(out + ((size_t)n * L + q) * C + hd * D + d) = v;
+      }
+    }
+  }
+}
+
 }  // namespace dmx
 

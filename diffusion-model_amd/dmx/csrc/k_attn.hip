@@ -12,4 +12,26 @@ void launch_attention_x3(int D, int wpe, int x1, const float* qkv, float* out, i
 #undef ATX
 }
 
+// D = 16 with the head resident in LDS (attention16_kernel): one block per (sample, head);
+// nw = 16 waves for L > 256, 8 for L <= 256.  More than 64 KB of dynamic LDS needs the
+// attribute, set once per instantiation (not a stream operation: capture-safe).
+template <int NW, int X1>
+static hipError_t go16(const float* qkv, float* out, int L, int C, int N, hipStream_t st) {
+  static size_t granted = 0;
+  const size_t bytes = att16_lds_bytes(L, X1);
+  if (bytes > granted) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention16_kernel<NW, X1>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) return e;
+    granted = bytes;
+  }
+  attention16_kernel<NW, X1><<<dim3(1, 4, N), NW * 64, bytes, st>>>(qkv, out, L, C);
+  return hipSuccess;
+}
+
+hipError_t launch_attention16(int nw, int x1, const float* qkv, float* out, int L, int C, int N, hipStream_t st) {
+  if (nw == 16) return x1 ? go16<16, 1>(qkv, out, L, C, N, st) : go16<16, 0>(qkv, out, L, C, N, st);
+  return x1 ? go16<8, 1>(qkv, out, L, C, N, st) : go16<8, 0>(qkv, out, L, C, N, st);
+}
+
 }  // namespace dmx
