@@ -174,21 +174,27 @@ def legs(nm, model, x, y, vals, mask, args, tables, seed):
     return out
 
 
-def train_leg(args, dev):
+def train_leg(args, dev, world=1, rank=0):
     """The training step of train_latent_cond.py:114-163 on the drop-ins, B = 32 224x224 synthetic
-    images: frozen VAE encode (micro-batches of 8, no_grad), t ~ U{1..1000}, add_noise, CFG dropout
-    (p = 0.1), UnetCondWithGeomHead forward + F.mse_loss + geom_lambda * masked_geom_mse, backward
-    (native dmx_train_backward), torch Adam(lr=1e-4) step.  Also the native forward + backward alone."""
+    images per GPU: frozen VAE encode (micro-batches of 8, no_grad), t ~ U{1..1000}, add_noise, CFG
+    dropout (p = 0.1), UnetCondWithGeomHead forward + F.mse_loss + geom_lambda * masked_geom_mse,
+    backward (native dmx_train_backward), torch Adam(lr=1e-4) step.  world > 1: data-parallel — every
+    rank its own batch, gradients averaged by dmx.distributed.GradAllReducer (bucketed async RCCL
+    all-reduces over xGMI) before the Adam step; value = images/s of the whole job (max over ranks).
+    Also the native forward + backward alone, and (world > 1) the gradient all-reduce alone."""
     import diff
+    from dmx import distributed as dd
     from dmx import synth
     from losses.geom_losses import masked_geom_mse
     from models.unet_cond_geom import UnetCondWithGeomHead
     from models.vae import VAE
     B = args.train_batch
-    g = torch.Generator().manual_seed(7)
+    g = torch.Generator().manual_seed(7 + rank)
     model = UnetCondWithGeomHead()
     model.load_state_dict(synth.unet_cond_geom_weights(0))
     model.to(dev).train()
+    dd.broadcast_module(model)
+    reducer = dd.GradAllReducer(model.parameters())
     vae = VAE()
     vae.load_state_dict(synth.vae_weights(1))
     vae.to(dev).eval()
@@ -213,19 +219,42 @@ def train_leg(args, dev):
         loss = F.mse_loss(eps, noise) + 0.5 * masked_geom_mse(geom, vals, mask * keep)
         opt.zero_grad(set_to_none=True)
         loss.backward()
+        reducer.reduce()
         opt.step()
         return loss
 
+    def synced():
+        torch.cuda.synchronize()
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    def max_over_ranks(v):
+        if world == 1:
+            return v
+        import torch.distributed as dist
+        e = torch.tensor([v], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        return float(e.item())
+
     for _ in range(2):
         step()
-    torch.cuda.synchronize()
+    synced()
     k = args.train_steps
     t0 = time.perf_counter()
     for _ in range(k):
         loss = step()
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / k
+    synced()
+    dt = max_over_ranks((time.perf_counter() - t0) / k)
     assert torch.isfinite(loss), "non-finite training loss"
+    ar_ms = None
+    if world > 1:  # the gradient all-reduce alone (grads of the last step still in place)
+        synced()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            reducer.reduce()
+        synced()
+        ar_ms = max_over_ranks((time.perf_counter() - t0) / k) * 1e3
     # native forward + backward alone (same shapes)
     nm = model.native()
     z = torch.randn((B, 4, 28, 28), generator=g).to(dev)
@@ -247,12 +276,17 @@ def train_leg(args, dev):
     t2 = time.perf_counter()
     fwd = (t1 - t0) / k
     fb = (t2 - t1) / k
-    return {"value": round(B / dt, 2), "unit": "training images/s (B=%d, 224x224 -> 28x28x4 latents)" % B,
-            "ms_per_step": round(dt * 1e3, 3), "steps": k,
+    res = {"value": round(world * B / dt, 2),
+           "unit": "training images/s (B=%d per GPU, 224x224 -> 28x28x4 latents)" % B,
+           "ms_per_step": round(dt * 1e3, 3), "steps": k, "n_gpus": world,
             "native_forward_ms": round(fwd * 1e3, 3), "native_backward_ms": round((fb - fwd) * 1e3, 3),
             "dtype": "f32 (exact fp32 MFMA GEMMs, fp32 everywhere)",
             "path": "train_latent_cond.py step on the drop-ins: VAE.encode x4, add_noise, forward, mse + "
                     "masked_geom_mse, loss.backward() (dmx_train_backward), torch Adam"}
+    if world > 1:
+        res["parallelism"] = f"data-parallel x{world}: bucketed async all-reduce of 93.7 MB fp32 gradients"
+        res["grad_allreduce_ms"] = round(ar_ms, 3)
+    return res
 
 
 MFMA_FAMILIES = ("igemm_x3_kernel", "igemm_x3g_kernel", "igemm_pp_kernel", "igemm_ad_kernel", "igemm_f32_kernel",
@@ -490,8 +524,8 @@ def main():
         out["config5"] = config5(nm, args, tables, seed)
     if world == 1 and args.legs_steps > 0:
         out.update(legs(nm, model, x, y, vals, mask, args, tables, seed))
-    if world == 1 and args.train_steps > 0:
-        out["train_step"] = train_leg(args, dev)
+    if args.train_steps > 0:
+        out["train_step"] = train_leg(args, dev, world, rank)
     if rank == 0:
         if not args.no_profile:
             xp = x.clone()

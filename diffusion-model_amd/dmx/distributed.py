@@ -1,4 +1,8 @@
-"""Sample-sharded multi-GPU sampling (one process per GPU, torch.distributed / RCCL).
+"""Multi-GPU paths (one process per GPU, torch.distributed / RCCL over xGMI).
+
+Sampling is sample-sharded; training is data-parallel (``GradAllReducer``, SURVEY.md §8f
+rank 2: every rank runs the train_latent_cond.py step on its own micro-batch, gradients
+are averaged with bucketed all-reduces before the optimizer step).
 
 The CFG loop has no cross-sample coupling (GroupNorm/LayerNorm are per sample), so a
 job of B samples is split into contiguous shards [start, end) per rank:
@@ -150,3 +154,75 @@ class ShardedCondSampler:
                 u8 = torch.empty((0, 8 * H, 8 * W, 3), dtype=torch.uint8, device=dev)
             return gather_rows(u8, B)
         return gather_rows(x, B)
+
+
+class GradAllReducer:
+    """Data-parallel gradient averaging for the training step (train_latent_cond.py:136-163 run
+    on every rank with its own batch).
+
+    After ``loss.backward()`` each rank holds dLoss_r/dθ of its local mean loss; ``reduce()``
+    replaces every ``p.grad`` with the mean over ranks, which is the gradient of the global-batch
+    mean loss when the local batches have equal sizes (the single-process reference trained on
+    the concatenated batch gives the same gradient up to fp32 summation order).  Then every rank
+    applies the same optimizer step to identical parameters (start them identical with
+    ``broadcast_module``), so replicas never drift.
+
+    Layout: parameters are packed, in reverse registration order (roughly the order the
+    backward finishes them), into buckets of about ``bucket_mb`` MB; each bucket is flattened
+    into one contiguous buffer and all-reduced asynchronously as soon as it is packed, so the
+    packing of bucket k+1 overlaps the wire time of bucket k (RCCL runs on its own stream).  On
+    xGMI's point-to-point links a ring all-reduce is per-link bound, so a few large buckets beat
+    many small ones; 25 MB gives 4 buckets for the 93.7 MB of U-Net gradients.
+
+    A gradient that is None on every rank stays None (the optimizer skips that parameter, as
+    with the reference's unused branches, e.g. ``cond_mlp`` without conditions); one that is
+    None on some ranks only is reduced as zeros there.  One tiny all-reduce of the presence
+    mask per step decides which."""
+
+    def __init__(self, params, bucket_mb: float = 25.0, group=None):
+        self.params = [p for p in params if p.requires_grad]
+        self.group = group
+        self.bucket_bytes = int(bucket_mb * (1 << 20))
+
+    def _buckets(self, present):
+        cur, size = [], 0
+        for i in reversed(range(len(self.params))):
+            if not present[i]:
+                continue
+            p = self.params[i]
+            cur.append(p)
+            size += p.numel() * p.element_size()
+            if size >= self.bucket_bytes:
+                yield cur
+                cur, size = [], 0
+        if cur:
+            yield cur
+
+    def reduce(self) -> None:
+        ws = dist.get_world_size(self.group) if dist.is_initialized() else 1
+        if ws == 1 or not self.params:
+            return
+        dev = self.params[0].device
+        on_host = dist.get_backend(self.group) == "gloo" and dev.type == "cuda"  # gloo: host buffers
+        mask = torch.tensor([p.grad is not None for p in self.params], dtype=torch.int32)
+        if not on_host:
+            mask = mask.to(dev)
+        dist.all_reduce(mask, op=dist.ReduceOp.MAX, group=self.group)
+        present = mask.cpu().tolist()
+        pending = []
+        for bucket in self._buckets(present):
+            grads = []
+            for p in bucket:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+                grads.append(p.grad)
+            flat = torch._utils._flatten_dense_tensors(grads)
+            if on_host:
+                flat = flat.cpu()
+            pending.append((dist.all_reduce(flat, group=self.group, async_op=True), flat, grads))
+        for work, flat, grads in pending:
+            work.wait()
+            flat = flat.to(dev) if on_host else flat
+            flat.div_(ws)
+            for g, r in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
+                g.copy_(r)

@@ -161,3 +161,54 @@ def _bad_gather(rank, world):
     except ValueError:
         return "ValueError"
     return "ok"
+
+
+# ---- data-parallel training: GradAllReducer ----------------------
+class _Toy(torch.nn.Module):
+    """Two-layer MLP with a branch used only by some ranks (`extra`) and one never used (`dead`)."""
+
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(3)
+        self.l1 = torch.nn.Linear(6, 16)
+        self.l2 = torch.nn.Linear(16, 3)
+        self.extra = torch.nn.Linear(6, 3)
+        self.dead = torch.nn.Linear(6, 3)
+
+    def forward(self, x, use_extra):
+        out = self.l2(torch.nn.functional.gelu(self.l1(x)))
+        return out + self.extra(x) if use_extra else out
+
+
+def _toy_batch():
+    g = torch.Generator().manual_seed(11)
+    return torch.randn((8, 6), generator=g), torch.randn((8, 3), generator=g)
+
+
+def _dp_grads(rank, world):
+    m = _Toy()
+    dd.broadcast_module(m)
+    x, y = _toy_batch()
+    s, e = dd.shard_range(8, world, rank)
+    loss = torch.nn.functional.mse_loss(m(x[s:e], use_extra=(rank == 0)), y[s:e])
+    loss.backward()
+    dd.GradAllReducer(m.parameters(), bucket_mb=0.0005).reduce()  # ~500 B buckets: several buckets
+    return {n: (None if p.grad is None else p.grad.clone()) for n, p in m.named_parameters()}
+
+
+def test_grad_allreduce_world2_equals_full_batch_mean():
+    """Averaged per-rank gradients == the gradient of the full-batch mean loss (equal shards);
+    a branch used on one rank only is reduced as zeros elsewhere; a never-used one stays None."""
+    res = run(_dp_grads)
+    m = _Toy()
+    x, y = _toy_batch()
+    # full-batch reference: rank 0's half uses `extra`, rank 1's half does not
+    out = torch.cat([m(x[:4], use_extra=True), m(x[4:], use_extra=False)])
+    torch.nn.functional.mse_loss(out, y).backward()
+    for n, p in m.named_parameters():
+        for r in (0, 1):
+            if p.grad is None:
+                assert res[r][n] is None, n
+            else:
+                assert torch.allclose(res[r][n], p.grad, rtol=1e-5, atol=1e-7), n
+    assert torch.equal(res[0]["l1.weight"], res[1]["l1.weight"])

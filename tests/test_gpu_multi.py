@@ -109,3 +109,66 @@ def test_sharded_world1_equals_diffuser_device_mode(cuda):
     ref_lat = d.sample_latent_cond(m, {1: 3, 3: 2}, z_shape=(4, 16, 16), vae=None, progress=False, cond=vals,
                                    cond_mask=mask)
     assert torch.equal(lat, ref_lat.cpu())
+
+
+# ---- data-parallel training step ----------------------------------
+def _train_job(rank, world, B=4):
+    """train_latent_cond.py's loss on this rank's half of a B = 4 batch (28x28x4 latents),
+    loss.backward() through dmx_train_backward, then GradAllReducer (gloo here, RCCL in bench).
+    geom mask all ones: the masked geom mean is then a plain mean, so the average of the two
+    half-batch gradients is exactly the full-batch gradient (up to fp32 summation order)."""
+    import torch.nn.functional as F
+    from dmx import distributed as dd
+    from dmx import synth
+    from losses.geom_losses import masked_geom_mse
+    from models.unet_cond_geom import UnetCondWithGeomHead
+    dev = torch.device("cuda:0")
+    m = UnetCondWithGeomHead()
+    m.load_state_dict(synth.unet_cond_geom_weights(0))
+    m.to(dev).train()
+    dd.broadcast_module(m)
+    g = torch.Generator().manual_seed(90)
+    z = torch.randn((B, 4, 28, 28), generator=g)
+    t = torch.randint(1, 1001, (B,), generator=g)
+    y = torch.randint(1, 4, (B,), generator=g)
+    vals = torch.rand((B, 12), generator=g)
+    noise = torch.randn((B, 4, 28, 28), generator=g)
+    mask = torch.ones((B, 12))
+    s, e = dd.shard_range(B, world, rank)
+    sl = [a[s:e].to(dev) for a in (z, t, y, vals, mask, noise)]
+    eps, geom = m(sl[0], sl[1], sl[2], cond_vals=sl[3], cond_mask=sl[4])
+    loss = F.mse_loss(eps, sl[5]) + 0.5 * masked_geom_mse(geom, sl[3], sl[4])
+    loss.backward()
+    dd.GradAllReducer(m.parameters()).reduce()
+    return {n: p.grad.detach().cpu() for n, p in m.named_parameters() if p.grad is not None}
+
+
+def _train_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, _train_job(rank, world)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_data_parallel_training_grads_world2_on_one_gpu(cuda):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_train_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    single = _train_job(0, 1)
+    assert set(res[0]) == set(res[1]) == set(single)
+    for n, gs in single.items():
+        assert torch.equal(res[0][n], res[1][n]), n  # replicas hold identical averaged gradients
+        err = float((res[0][n] - gs).norm() / gs.norm().clamp_min(1e-30))
+        assert err <= 1e-4, (n, err)  # the single-GPU native-gradient bound (test_gpu_train.py)
