@@ -561,7 +561,7 @@ __host__ __device__ inline size_t att16_lds_bytes(int L, int x1) {
 
 template <int NW, int X1 = 0>
 __global__ __launch_bounds__(NW * 64) void attention16_kernel(const float* qkv, float* out, int L, int C) {
-  constexpr int D = 16, KC = 64;
+  constexpr int D = 16;
   extern __shared__ __attribute__((aligned(16))) _Float16 att_lds[];
   const int Lp = att16_lp(L), VS = Lp + 8;
   _Float16* Kh = att_lds;
@@ -640,96 +640,93 @@ __global__ __launch_bounds__(NW * 64) void attention16_kernel(const float* qkv, 
         ql[j + 4] = (_Float16)(vb - (float)hb);
       }
     }
-    floatx16 o;
+    // Lazily rescaled online softmax: the first S^T MFMA of a tile takes C = -mref, so scores
+    // leave the matrix cores already shifted by the running reference max (no per-score
+    // subtract), and P = exp2(s - mref).  The reference moves — rescaling O, whose ones row is
+    // the denominator — only on a tile's first chunk or when a chunk's max exceeds it by more
+    // than TAU (P <= 2^TAU in between: exact in fp32 and in the f16 hi / lo split).  O / l does
+    // not depend on the reference.
+    constexpr float TAU = 8.f;
+    floatx16 o, negm;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) o[r] = 0.f;
-    float mrun = -INFINITY;
-    for (int c0 = 0; c0 < L; c0 += KC) {
-      floatx16 sc[2];
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sc[kt][r] = 0.f;
-        const int krow = (c0 + kt * 32 + fr) * D + 8 * fh;
+    for (int r = 0; r < 16; ++r) o[r] = negm[r] = 0.f;
+    float mref = 0.f;
+    for (int c0 = 0; c0 < L; c0 += 32) {  // 32-key chunks: one S^T tile live (register budget)
+      floatx16 sc;
+      {
+        const int krow = (c0 + fr) * D + 8 * fh;
         const half8 kh = *reinterpret_cast<const half8*>(&Kh[krow]);
         if constexpr (!X1) {
           const half8 kl = *reinterpret_cast<const half8*>(&Kl[krow]);
-          sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kl, qh, sc[kt], 0, 0, 0);
-          sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, ql, sc[kt], 0, 0, 0);
+          sc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kl, qh, negm, 0, 0, 0);
+          sc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, ql, sc, 0, 0, 0);
+          sc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, qh, sc, 0, 0, 0);
+        } else {
+          sc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, qh, negm, 0, 0, 0);
         }
-        sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, qh, sc[kt], 0, 0, 0);
       }
       const int nvalid = L - c0;
-      if (nvalid < KC) {  // ragged last chunk only (uniform branch)
+      if (nvalid < 32) {  // ragged last chunk only (uniform branch)
 #pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int key = kt * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
-            if (key >= nvalid) sc[kt][r] = -INFINITY;
-          }
+        for (int r = 0; r < 16; ++r)
+          if ((r & 3) + 8 * (r >> 2) + 4 * fh >= nvalid) sc[r] = -INFINITY;
       }
-      float mx = sc[0][0];
+      float mx = sc[0];
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[kt][r]);
+      for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sc[r]);
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(mrun, mx);
-      const float alpha = __builtin_amdgcn_exp2f(mrun - mnew);
-      mrun = mnew;
-      // scalar f32 VALU only: packed v_pk_add / v_pk_mul beside MFMAs cost far more issue time
-      // than their two scalar halves (MI355X_MICROARCH.md, constants table)
-      u32x4 phu[2][2], plu[2][2];
+      if (c0 == 0 || mx > TAU) {  // move the reference to this chunk's max (rare after the first)
+        const float alpha = __builtin_amdgcn_exp2f(-mx);
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+        for (int r = 0; r < 16; ++r) o[r] *= alpha;
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
+        for (int r = 0; r < 16; ++r) sc[r] -= mx;
+        mref += mx;
 #pragma unroll
-          for (int jp = 0; jp < 4; ++jp) {
-            f32x2 v;
-            v.x = __builtin_amdgcn_exp2f(sc[kt][8 * s + 2 * jp] - mnew);
-            v.y = __builtin_amdgcn_exp2f(sc[kt][8 * s + 2 * jp + 1] - mnew);
-            unsigned h, l;
-            if constexpr (X1) {
-              h = __builtin_bit_cast(unsigned, __builtin_convertvector(v, half2v));
-              l = 0u;
-            } else {
-              split2(v, h, l);
-            }
-            phu[kt][s][jp] = h;
-            plu[kt][s][jp] = l;
+        for (int r = 0; r < 16; ++r) negm[r] = -mref;
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        u32x4 phu, plu;
+#pragma unroll
+        for (int jp = 0; jp < 4; ++jp) {
+          f32x2 v;
+          v.x = __builtin_amdgcn_exp2f(sc[8 * s + 2 * jp]);
+          v.y = __builtin_amdgcn_exp2f(sc[8 * s + 2 * jp + 1]);
+          unsigned h, l;
+          if constexpr (X1) {
+            h = __builtin_bit_cast(unsigned, __builtin_convertvector(v, half2v));
+            l = 0u;
+          } else {
+            split2(v, h, l);
           }
+          phu[jp] = h;
+          plu[jp] = l;
+        }
+        const half8 ph = __builtin_bit_cast(half8, phu);
+        const half8 pl = __builtin_bit_cast(half8, plu);
+        const int k0 = c0 + 16 * s + 4 * fh;
+        half8 vh, vl;
+        const half4 a0 = *reinterpret_cast<const half4*>(vrh + k0);
+        const half4 a1 = *reinterpret_cast<const half4*>(vrh + k0 + 8);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[r] *= alpha;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const half8 ph = __builtin_bit_cast(half8, phu[kt][s]);
-          const half8 pl = __builtin_bit_cast(half8, plu[kt][s]);
-          const int k0 = c0 + kt * 32 + 16 * s + 4 * fh;
-          half8 vh, vl;
-          const half4 a0 = *reinterpret_cast<const half4*>(vrh + k0);
-          const half4 a1 = *reinterpret_cast<const half4*>(vrh + k0 + 8);
+        for (int j = 0; j < 4; ++j) {
+          vh[j] = a0[j];
+          vh[j + 4] = a1[j];
+        }
+        if constexpr (!X1) {
+          const half4 b0 = *reinterpret_cast<const half4*>(vrl + k0);
+          const half4 b1 = *reinterpret_cast<const half4*>(vrl + k0 + 8);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            vh[j] = a0[j];
-            vh[j + 4] = a1[j];
+            vl[j] = b0[j];
+            vl[j + 4] = b1[j];
           }
-          if constexpr (!X1) {
-            const half4 b0 = *reinterpret_cast<const half4*>(vrl + k0);
-            const half4 b1 = *reinterpret_cast<const half4*>(vrl + k0 + 8);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              vl[j] = b0[j];
-              vl[j + 4] = b1[j];
-            }
-            o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph, o, 0, 0, 0);
-            o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, pl, o, 0, 0, 0);
-          }
-          o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, o, 0, 0, 0);
+          o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vl, ph, o, 0, 0, 0);
+          o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, pl, o, 0, 0, 0);
         }
+        o = __builtin_amdgcn_mfma_f32_32x32x16_f16(vh, ph, o, 0, 0, 0);
+      }
     }
     const float inv = 1.0f / __shfl(o[8], fr, 64);  // O^T row 16 (the ones row) = the denominator
     if (q < L) {
