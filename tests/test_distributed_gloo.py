@@ -19,12 +19,31 @@ def _free_port():
     return p
 
 
+class _ByValue:
+    """A tensor shipped as a numpy array."""
+
+    def __init__(self, a):
+        self.a = a
+
+
+def _convert(obj, f):
+    if isinstance(obj, _ByValue):
+        return f(obj)
+    if isinstance(obj, dict):
+        return {k: _convert(v, f) for k, v in obj.items()}
+    if isinstance(obj, (list, tuple)):
+        return type(obj)(_convert(v, f) for v in obj)
+    return f(obj)
+
+
 def _worker(rank, world, port, fn, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        q.put((rank, fn(rank, world)))
+        # tensors travel by value (numpy): a torch tensor would be a shared-memory fd that the
+        # parent can only open while this process is still alive
+        q.put((rank, _convert(fn(rank, world), lambda v: _ByValue(v.numpy()) if torch.is_tensor(v) else v)))
     finally:
         dist.destroy_process_group()
 
@@ -36,7 +55,8 @@ def run(fn, world=2):
     procs = [ctx.Process(target=_worker, args=(r, world, port, fn, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=120) for _ in procs)
+    back = (lambda v: torch.from_numpy(v.a) if isinstance(v, _ByValue) else v)
+    res = {r: _convert(v, back) for r, v in (q.get(timeout=120) for _ in procs)}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -53,7 +53,10 @@ def _worker(rank, world, port, mode, decode, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        q.put((rank, _job(mode, decode)))
+        out = _job(mode, decode)
+        # by value (numpy): a torch tensor would travel as a shared-memory fd that the parent can
+        # only open while this process is still alive
+        q.put((rank, None if out is None else out.numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -66,7 +69,7 @@ def _run2(mode, decode):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, mode, decode, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=300) for _ in procs)
+    res = {r: (None if a is None else torch.from_numpy(a)) for r, a in (q.get(timeout=300) for _ in procs)}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -154,7 +157,7 @@ def _train_worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        q.put((rank, _train_job(rank, world)))
+        q.put((rank, {n: g.numpy() for n, g in _train_job(rank, world).items()}))  # by value, see _worker
     finally:
         dist.destroy_process_group()
 
@@ -167,7 +170,7 @@ def test_data_parallel_training_grads_world2_on_one_gpu(cuda):
     procs = [ctx.Process(target=_train_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=300) for _ in procs)
+    res = {r: {n: torch.from_numpy(a) for n, a in g.items()} for r, g in (q.get(timeout=300) for _ in procs)}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
