@@ -209,35 +209,54 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int fr = lane & 31, fh = lane >> 5;
+  // Fragments of k16-step s+1 are read from LDS while step s's MFMAs issue (double-buffered
+  // fragment registers, interleave pinned with sched_group_barrier), so only the first step of
+  // a K-tile waits on LDS latency.
   auto compute = [&](int buf) {
-#pragma unroll
-    for (int s = 0; s < BK / 16; ++s) {
-      half8 ah[TM], al[TM], bh[TN], bl[TN];
+    constexpr int S = BK / 16, NR = (X1 ? 1 : 2) * (TM + TN), NM = (X1 ? 1 : 3) * TM * TN;
+    half8 ah[2][TM], al[2][TM], bh[2][TN], bl[2][TN];
+    auto ldf = [&](int s, int d) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * WM + i * 32 + fr;
-        ah[i] = *reinterpret_cast<const half8*>(&Ah[buf][row][16 * s + 8 * fh]);
-        if constexpr (!X1) al[i] = *reinterpret_cast<const half8*>(&Al[buf][row][16 * s + 8 * fh]);
+        ah[d][i] = *reinterpret_cast<const half8*>(&Ah[buf][row][16 * s + 8 * fh]);
+        if constexpr (!X1) al[d][i] = *reinterpret_cast<const half8*>(&Al[buf][row][16 * s + 8 * fh]);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * WN + j * 32 + fr;
-        bh[j] = *reinterpret_cast<const half8*>(&Bhs[buf][row][16 * s + 8 * fh]);
-        if constexpr (!X1) bl[j] = *reinterpret_cast<const half8*>(&Bls[buf][row][16 * s + 8 * fh]);
+        bh[d][j] = *reinterpret_cast<const half8*>(&Bhs[buf][row][16 * s + 8 * fh]);
+        if constexpr (!X1) bl[d][j] = *reinterpret_cast<const half8*>(&Bls[buf][row][16 * s + 8 * fh]);
       }
+    };
+    ldf(0, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);  // step 0's reads first
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int d = s & 1;
+      if (s + 1 < S) ldf(s + 1, d ^ 1);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           if constexpr (!X1) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i], bh[j], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[d][i], bh[d][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[d][i], bl[d][j], acc[i][j], 0, 0, 0);
           }
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[d][i], bh[d][j], acc[i][j], 0, 0, 0);
         }
+      if (s + 1 < S) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {  // one next-step read after each of the first NR MFMAs
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, NM - NR, 0);
+      } else {
+        __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
+      }
     }
   };
-
   int kbeg = 0, nK = p.Kpad / BK;
   if constexpr (EPI == EPI_PARTIAL) {
     kbeg = blockIdx.z * p.ksplit;
