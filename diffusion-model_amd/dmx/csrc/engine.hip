@@ -747,7 +747,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   const bool x1 = x3 && R.m->prec == 2;  // config-4 fp16: one MFMA on the hi planes
   // 512-thread ping-pong kernel (256-row tiles) for the large f16-plane convs
   const bool pp = pp_enabled() && x3 && epi == EPI_STATS && cw.phases == 1 && s.C >= 32 && ash != nullptr &&
-                  cdiv(M, 256) * cdiv(cw.cout, bn) >= 256;
+                  (H * W) % 32 == 0 && cdiv(M, 256) * cdiv(cw.cout, bn) >= 256;  // 32-row GN partials
   const int bk = pp ? 32 : x3 ? 64 : IG_BK;
   const int nkt = cw.kpad / bk;
   int splits = 1, ksplit = nkt;
