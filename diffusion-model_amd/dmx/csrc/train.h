@@ -582,11 +582,17 @@ static __global__ void upcat_bwd_kernel(const float* dcat, float* dskip, float* 
 // attn_dkv_kernel: one thread per key, queries streamed through LDS.
 // qkv: [N][L][3C] (q | k | v, head h at columns h*D), o / dO: [N][L][C]; dqkv: [N][L][3C].
 // ---------------------------------------------------------------------------
-template <int D>
-__global__ __launch_bounds__(64) void attn_rowstats_kernel(const float* qkv, const float* o, const float* dout,
-                                                           float* st, int L, int C) {
-  __shared__ float ks[64][D];
-  const int hd = blockIdx.y, n = blockIdx.z, i = blockIdx.x * 64 + threadIdx.x;
+// KS waves per block split the streamed dimension (keys for rowstats / dq, queries for dkv):
+// wave w stages and walks tiles w, w + KS, ... in its own LDS slice, and the per-wave partial
+// results are combined in wave order at the end (deterministic).  KS = 1 is one wave per row
+// block; KS = 4 gives the GPU 4x the waves for the small per-(sample, head) grids of training.
+template <int D, int KS>
+__global__ __launch_bounds__(64 * KS) void attn_rowstats_kernel(const float* qkv, const float* o, const float* dout,
+                                                                float* st, int L, int C) {
+  __shared__ float ks[KS][64][D];
+  __shared__ float red[KS][64][2];
+  const int w = threadIdx.x >> 6, lt = threadIdx.x & 63;
+  const int hd = blockIdx.y, n = blockIdx.z, i = blockIdx.x * 64 + lt;
   const size_t rs = 3 * (size_t)C;
   const float* base = qkv + (size_t)n * L * rs;
   const float sc = 1.0f / sqrtf((float)D);
@@ -594,17 +600,20 @@ __global__ __launch_bounds__(64) void attn_rowstats_kernel(const float* qkv, con
 #pragma unroll
   for (int d = 0; d < D; ++d) q[d] = i < L ? base[(size_t)i * rs + hd * D + d] * sc : 0.f;
   float m = -INFINITY, l = 0.f;
-  for (int j0 = 0; j0 < L; j0 += 64) {
-    __syncthreads();
-    for (int e = threadIdx.x; e < 64 * D; e += 64) {
+  const int nt = (L + 63) / 64;
+  for (int t = w; t < nt; t += KS) {
+    const int j0 = t * 64;
+    __builtin_amdgcn_wave_barrier();
+    for (int e = lt; e < 64 * D; e += 64) {
       const int j = e / D, d = e % D;
-      ks[j][d] = j0 + j < L ? base[(size_t)(j0 + j) * rs + C + hd * D + d] : 0.f;
+      ks[w][j][d] = j0 + j < L ? base[(size_t)(j0 + j) * rs + C + hd * D + d] : 0.f;
     }
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     for (int j = 0; j < 64 && j0 + j < L; ++j) {
       float s = 0.f;
 #pragma unroll
-      for (int d = 0; d < D; ++d) s += q[d] * ks[j][d];
+      for (int d = 0; d < D; ++d) s += q[d] * ks[w][j][d];
       if (s > m) {
         l = l * expf(m - s) + 1.f;
         m = s;
@@ -612,24 +621,38 @@ __global__ __launch_bounds__(64) void attn_rowstats_kernel(const float* qkv, con
         l += expf(s - m);
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   }
-  if (i < L) {
+  red[w][lt][0] = m;
+  red[w][lt][1] = l;
+  __syncthreads();
+  if (w == 0 && i < L) {
+    float M = red[0][lt][0];
+#pragma unroll
+    for (int u = 1; u < KS; ++u) M = fmaxf(M, red[u][lt][0]);
+    float Ls = 0.f;
+#pragma unroll
+    for (int u = 0; u < KS; ++u) {
+      const float mu = red[u][lt][0];
+      if (mu > -INFINITY) Ls += red[u][lt][1] * expf(mu - M);
+    }
     float dl = 0.f;
     const size_t ob = ((size_t)n * L + i) * C + hd * D;
 #pragma unroll
     for (int d = 0; d < D; ++d) dl += dout[ob + d] * o[ob + d];
-    float* s = st + (((size_t)n * 4 + hd) * L + i) * 3;
-    s[0] = m;
-    s[1] = l;
-    s[2] = dl;
+    float* so = st + (((size_t)n * 4 + hd) * L + i) * 3;
+    so[0] = M;
+    so[1] = Ls;
+    so[2] = dl;
   }
 }
 
-template <int D>
-__global__ __launch_bounds__(64) void attn_dq_kernel(const float* qkv, const float* dout, const float* st, float* dqkv,
-                                                     int L, int C) {
-  __shared__ float ks[64][D], vs[64][D];
-  const int hd = blockIdx.y, n = blockIdx.z, i = blockIdx.x * 64 + threadIdx.x;
+template <int D, int KS>
+__global__ __launch_bounds__(64 * KS) void attn_dq_kernel(const float* qkv, const float* dout, const float* st,
+                                                          float* dqkv, int L, int C) {
+  __shared__ float ks[KS][64][D], vs[KS][64][D];
+  const int w = threadIdx.x >> 6, lt = threadIdx.x & 63;
+  const int hd = blockIdx.y, n = blockIdx.z, i = blockIdx.x * 64 + lt;
   const size_t rs = 3 * (size_t)C;
   const float* base = qkv + (size_t)n * L * rs;
   const float sc = 1.0f / sqrtf((float)D);
@@ -643,25 +666,44 @@ __global__ __launch_bounds__(64) void attn_dq_kernel(const float* qkv, const flo
   }
   const float* s3 = st + (((size_t)n * 4 + hd) * L + min(i, L - 1)) * 3;
   const float m = s3[0], il = 1.0f / s3[1], dl = s3[2];
-  for (int j0 = 0; j0 < L; j0 += 64) {
-    __syncthreads();
-    for (int e = threadIdx.x; e < 64 * D; e += 64) {
+  const int nt = (L + 63) / 64;
+  for (int t = w; t < nt; t += KS) {
+    const int j0 = t * 64;
+    __builtin_amdgcn_wave_barrier();
+    for (int e = lt; e < 64 * D; e += 64) {
       const int j = e / D, d = e % D;
       const bool ok = j0 + j < L;
-      ks[j][d] = ok ? base[(size_t)(j0 + j) * rs + C + hd * D + d] : 0.f;
-      vs[j][d] = ok ? base[(size_t)(j0 + j) * rs + 2 * C + hd * D + d] : 0.f;
+      ks[w][j][d] = ok ? base[(size_t)(j0 + j) * rs + C + hd * D + d] : 0.f;
+      vs[w][j][d] = ok ? base[(size_t)(j0 + j) * rs + 2 * C + hd * D + d] : 0.f;
     }
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     for (int j = 0; j < 64 && j0 + j < L; ++j) {
       float s = 0.f, dp = 0.f;
 #pragma unroll
       for (int d = 0; d < D; ++d) {
-        s += q[d] * ks[j][d];
-        dp += g[d] * vs[j][d];
+        s += q[d] * ks[w][j][d];
+        dp += g[d] * vs[w][j][d];
       }
       const float ds = expf(s - m) * il * (dp - dl);
 #pragma unroll
-      for (int d = 0; d < D; ++d) dq[d] += ds * ks[j][d];
+      for (int d = 0; d < D; ++d) dq[d] += ds * ks[w][j][d];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+  if constexpr (KS > 1) {  // combine the waves' partial dQ in wave order (reuse the K slices)
+    __syncthreads();
+    float* red = &ks[0][0][0];  // [KS][64][D] floats
+#pragma unroll
+    for (int d = 0; d < D; ++d) red[(w * 64 + lt) * D + d] = dq[d];
+    __syncthreads();
+    if (w != 0) return;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      float a = red[lt * D + d];
+#pragma unroll
+      for (int u = 1; u < KS; ++u) a += red[(u * 64 + lt) * D + d];
+      dq[d] = a;
     }
   }
   if (i < L) {
@@ -671,11 +713,12 @@ __global__ __launch_bounds__(64) void attn_dq_kernel(const float* qkv, const flo
   }
 }
 
-template <int D>
-__global__ __launch_bounds__(64) void attn_dkv_kernel(const float* qkv, const float* dout, const float* st, float* dqkv,
-                                                      int L, int C) {
-  __shared__ float qs[64][D], gs[64][D], ss[64][3];
-  const int hd = blockIdx.y, n = blockIdx.z, j = blockIdx.x * 64 + threadIdx.x;
+template <int D, int KS>
+__global__ __launch_bounds__(64 * KS) void attn_dkv_kernel(const float* qkv, const float* dout, const float* st,
+                                                           float* dqkv, int L, int C) {
+  __shared__ float qs[KS][64][D], gs[KS][64][D], ss[KS][64][3];
+  const int w = threadIdx.x >> 6, lt = threadIdx.x & 63;
+  const int hd = blockIdx.y, n = blockIdx.z, j = blockIdx.x * 64 + lt;
   const size_t rs = 3 * (size_t)C;
   const float* base = qkv + (size_t)n * L * rs;
   const float sc = 1.0f / sqrtf((float)D);
@@ -686,35 +729,62 @@ __global__ __launch_bounds__(64) void attn_dkv_kernel(const float* qkv, const fl
     v[d] = j < L ? base[(size_t)j * rs + 2 * C + hd * D + d] : 0.f;
     dk[d] = dv[d] = 0.f;
   }
-  for (int i0 = 0; i0 < L; i0 += 64) {
-    __syncthreads();
-    for (int e = threadIdx.x; e < 64 * D; e += 64) {
+  const int nt = (L + 63) / 64;
+  for (int t = w; t < nt; t += KS) {
+    const int i0 = t * 64;
+    __builtin_amdgcn_wave_barrier();
+    for (int e = lt; e < 64 * D; e += 64) {
       const int i = e / D, d = e % D;
       const bool ok = i0 + i < L;
-      qs[i][d] = ok ? base[(size_t)(i0 + i) * rs + hd * D + d] * sc : 0.f;
-      gs[i][d] = ok ? dout[((size_t)n * L + i0 + i) * C + hd * D + d] : 0.f;
+      qs[w][i][d] = ok ? base[(size_t)(i0 + i) * rs + hd * D + d] * sc : 0.f;
+      gs[w][i][d] = ok ? dout[((size_t)n * L + i0 + i) * C + hd * D + d] : 0.f;
     }
-    if (i0 + (int)threadIdx.x < L) {
-      const float* s3 = st + (((size_t)n * 4 + hd) * L + i0 + threadIdx.x) * 3;
-      ss[threadIdx.x][0] = s3[0];
-      ss[threadIdx.x][1] = 1.0f / s3[1];
-      ss[threadIdx.x][2] = s3[2];
+    if (i0 + lt < L) {
+      const float* s3 = st + (((size_t)n * 4 + hd) * L + i0 + lt) * 3;
+      ss[w][lt][0] = s3[0];
+      ss[w][lt][1] = 1.0f / s3[1];
+      ss[w][lt][2] = s3[2];
     }
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     for (int i = 0; i < 64 && i0 + i < L; ++i) {
       float s = 0.f, dp = 0.f;
 #pragma unroll
       for (int d = 0; d < D; ++d) {
-        s += qs[i][d] * k[d];
-        dp += gs[i][d] * v[d];
+        s += qs[w][i][d] * k[d];
+        dp += gs[w][i][d] * v[d];
       }
-      const float pr = expf(s - ss[i][0]) * ss[i][1];
-      const float ds = pr * (dp - ss[i][2]);
+      const float pr = expf(s - ss[w][i][0]) * ss[w][i][1];
+      const float ds = pr * (dp - ss[w][i][2]);
 #pragma unroll
       for (int d = 0; d < D; ++d) {
-        dv[d] += pr * gs[i][d];
-        dk[d] += ds * qs[i][d];  // qs already carries the 1/sqrt(D)
+        dv[d] += pr * gs[w][i][d];
+        dk[d] += ds * qs[w][i][d];  // qs already carries the 1/sqrt(D)
       }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  }
+  if constexpr (KS > 1) {  // combine the waves' partial dK / dV in wave order
+    __syncthreads();
+    float* rk = &qs[0][0][0];
+    float* rv = &gs[0][0][0];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      rk[(w * 64 + lt) * D + d] = dk[d];
+      rv[(w * 64 + lt) * D + d] = dv[d];
+    }
+    __syncthreads();
+    if (w != 0) return;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      float a = rk[lt * D + d], b = rv[lt * D + d];
+#pragma unroll
+      for (int u = 1; u < KS; ++u) {
+        a += rk[(u * 64 + lt) * D + d];
+        b += rv[(u * 64 + lt) * D + d];
+      }
+      dk[d] = a;
+      dv[d] = b;
     }
   }
   if (j < L) {

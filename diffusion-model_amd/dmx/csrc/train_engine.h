@@ -584,18 +584,18 @@ static void attn_core_bwd(Run& R, const float* qkv, const float* o, const float*
   const int D = C / 4;
   const dim3 grid(cdiv(L, 64), 4, N);
   R.begin("attn_bwd_kernels<" + std::to_string(D) + ">", 3.0 * 4.0 * N * (double)L * L * C, 4.0 * N * (double)L * 6 * C);
-  if (D == 16) {
-    attn_rowstats_kernel<16><<<grid, 64, 0, R.st>>>(qkv, o, dout, st, L, C);
-    attn_dq_kernel<16><<<grid, 64, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
-    attn_dkv_kernel<16><<<grid, 64, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
+  if (D == 16) {  // 4 waves per block split the streamed dimension (training grids are small)
+    attn_rowstats_kernel<16, 4><<<grid, 256, 0, R.st>>>(qkv, o, dout, st, L, C);
+    attn_dq_kernel<16, 4><<<grid, 256, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
+    attn_dkv_kernel<16, 4><<<grid, 256, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
   } else if (D == 32) {
-    attn_rowstats_kernel<32><<<grid, 64, 0, R.st>>>(qkv, o, dout, st, L, C);
-    attn_dq_kernel<32><<<grid, 64, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
-    attn_dkv_kernel<32><<<grid, 64, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
+    attn_rowstats_kernel<32, 4><<<grid, 256, 0, R.st>>>(qkv, o, dout, st, L, C);
+    attn_dq_kernel<32, 4><<<grid, 256, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
+    attn_dkv_kernel<32, 4><<<grid, 256, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
   } else if (D == 64) {
-    attn_rowstats_kernel<64><<<grid, 64, 0, R.st>>>(qkv, o, dout, st, L, C);
-    attn_dq_kernel<64><<<grid, 64, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
-    attn_dkv_kernel<64><<<grid, 64, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
+    attn_rowstats_kernel<64, 1><<<grid, 64, 0, R.st>>>(qkv, o, dout, st, L, C);
+    attn_dq_kernel<64, 1><<<grid, 64, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
+    attn_dkv_kernel<64, 1><<<grid, 64, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
   } else {
     throw Error(DMX_E_INTERNAL, "attention backward: unsupported head dim");
   }
