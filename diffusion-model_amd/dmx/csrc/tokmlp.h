@@ -21,6 +21,10 @@
 #include "common.h"
 #include "igemm_x3.h"
 
+#ifndef DMX_TOK_PD
+#define DMX_TOK_PD 8  // k16 steps of B fragments in flight in tok_gemm (L2 latency cover)
+#endif
+
 namespace dmx {
 
 struct TokW {                 // one Linear in the x3 B layout
@@ -150,7 +154,7 @@ DMX_DEV void tok_rows(const float* src, int ld, int m0, int M, const float* g, c
 template <int C, int NT, int X1 = 0>
 DMX_DEV void tok_gemm(const _Float16 (*Ah)[C + 8], const _Float16 (*Al)[C + 8], const TokW& w, int nw,
                       floatx16 (&acc)[NT], int arow0, int fr, int fh) {
-  constexpr int S = C / 16, PD = S < 4 ? S : 4;
+  constexpr int S = C / 16, PD = S < DMX_TOK_PD ? S : DMX_TOK_PD;
 #pragma unroll
   for (int j = 0; j < NT; ++j)
 #pragma unroll
