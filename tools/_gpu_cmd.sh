@@ -1,2 +1,7 @@
-timeout -k 10 300 python -u -m pytest tests/test_gpu_train.py tests/test_gpu_poison.py -q -x --timeout 250 > gpurun_out/pt.log 2>&1; tail -1 gpurun_out/pt.log
-timeout -k 10 300 python bench.py --steps 5 --warmup 2 --cpu-steps 0 --config4-steps 0 --config5-steps 0 --legs-steps 0 --png-steps 0 --train-steps 10 --no-profile > gpurun_out/tb.log 2>&1; python -c "import json;d=json.loads(open('gpurun_out/tb.log').read().strip().splitlines()[-1]);print(json.dumps(d['train_step']))"
+ROUNDS=1 bash tools/ab_lib.sh libdmx.so libg4.so libg1.so
+python -c "
+import json
+for l in ('libdmx','libg4','libg1'):
+    for r in json.load(open('gpurun_out/bd_%s.json' % l))['records']:
+        if r['layer']=='embed': print(l, round(r['ms']*1000,1))
+"
