@@ -202,33 +202,43 @@ class _Toy(torch.nn.Module):
 
 def _toy_batch():
     g = torch.Generator().manual_seed(11)
-    return torch.randn((8, 6), generator=g), torch.randn((8, 3), generator=g)
+    return torch.randn((12, 6), generator=g), torch.randn((12, 3), generator=g)
 
 
-def _dp_grads(rank, world):
+def _dp_grads(rank, world, bucket_mb):
     m = _Toy()
     dd.broadcast_module(m)
     x, y = _toy_batch()
-    s, e = dd.shard_range(8, world, rank)
+    s, e = dd.shard_range(12, world, rank)
     loss = torch.nn.functional.mse_loss(m(x[s:e], use_extra=(rank == 0)), y[s:e])
     loss.backward()
-    dd.GradAllReducer(m.parameters(), bucket_mb=0.0005).reduce()  # ~500 B buckets: several buckets
+    dd.GradAllReducer(m.parameters(), bucket_mb=bucket_mb).reduce()
     return {n: (None if p.grad is None else p.grad.clone()) for n, p in m.named_parameters()}
 
 
-def test_grad_allreduce_world2_equals_full_batch_mean():
+def _dp_small_buckets(rank, world):
+    return _dp_grads(rank, world, 0.0005)  # ~500 B buckets: several buckets, async in flight together
+
+
+def _dp_one_bucket(rank, world):
+    return _dp_grads(rank, world, 25.0)
+
+
+@pytest.mark.parametrize("fn,world", [(_dp_small_buckets, 2), (_dp_one_bucket, 2), (_dp_small_buckets, 3)])
+def test_grad_allreduce_equals_full_batch_mean(fn, world):
     """Averaged per-rank gradients == the gradient of the full-batch mean loss (equal shards);
     a branch used on one rank only is reduced as zeros elsewhere; a never-used one stays None."""
-    res = run(_dp_grads)
+    res = run(fn, world)
     m = _Toy()
     x, y = _toy_batch()
-    # full-batch reference: rank 0's half uses `extra`, rank 1's half does not
-    out = torch.cat([m(x[:4], use_extra=True), m(x[4:], use_extra=False)])
+    per = 12 // world  # full-batch reference: rank 0's shard uses `extra`, the others do not
+    out = torch.cat([m(x[:per], use_extra=True), m(x[per:], use_extra=False)])
     torch.nn.functional.mse_loss(out, y).backward()
     for n, p in m.named_parameters():
-        for r in (0, 1):
+        for r in range(world):
             if p.grad is None:
                 assert res[r][n] is None, n
             else:
                 assert torch.allclose(res[r][n], p.grad, rtol=1e-5, atol=1e-7), n
-    assert torch.equal(res[0]["l1.weight"], res[1]["l1.weight"])
+    for r in range(1, world):
+        assert torch.equal(res[0]["l1.weight"], res[r]["l1.weight"])
