@@ -297,6 +297,10 @@ struct dmx_model {
   // tensors, in finalize order; the f16 planes of the split GEMMs are re-derived lazily
   // (planes_stale) before the next split-precision launch.
   std::vector<std::function<void(hipStream_t)>> jobs;
+  std::vector<dmx::CopyJob> copies;     // parameter copies and weight repacks, replayed batched
+  std::vector<dmx::RepackJob> repacks;  // (one launch each) by dmx_model_refresh
+  void* job_tables = nullptr;           // device copies of the two tables
+  size_t job_tables_n = 0;              // copies.size() + repacks.size() when uploaded
   bool planes_stale = false;
   unsigned* amax = nullptr;  // absmax scratch of split_planes
   // training (train_engine.h): tape of the last dmx_train_forward, its workspace and the
@@ -386,7 +390,8 @@ struct Packer {
     for (auto s : t.second) n *= (size_t)s;
     float* d = alloc(n);
     const float* src = t.first;
-    job([=](hipStream_t s) { HIPCHK(hipMemcpyAsync(d, src, n * sizeof(float), hipMemcpyDeviceToDevice, s)); });
+    HIPCHK(hipMemcpyAsync(d, src, n * sizeof(float), hipMemcpyDeviceToDevice, st));
+    m->copies.push_back(CopyJob{d, src, n});  // replayed batched by dmx_model_refresh
     return d;
   }
   Vec vec(const std::string& name) { return Vec{copy(name)}; }
@@ -413,12 +418,13 @@ struct Packer {
     return m->amax;
   }
   void repack(float* dst, const float* src, int kind, int P, int npad, int kpad, int cout, int cin, int ks) {
-    job([=](hipStream_t s) {
-      const size_t total = (size_t)P * npad * kpad;
-      const int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
-      repack_kernel<<<blocks, 256, 0, s>>>(dst, src, kind, P, npad, kpad, cout, cin, ks);
-      HIPCHK(hipGetLastError());
-    });
+    const size_t total = (size_t)P * npad * kpad;
+    const int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
+    repack_kernel<<<blocks, 256, 0, st>>>(dst, src, kind, P, npad, kpad, cout, cin, ks);
+    HIPCHK(hipGetLastError());
+    // replayed batched by dmx_model_refresh, after the recorded jobs (which produce the
+    // padded / flipped / transposed sources some repacks read)
+    m->repacks.push_back(RepackJob{dst, src, kind, P, npad, kpad, cout, cin, ks});
   }
   // Conv2d [cout][cin][ks][ks]; channel-padded to cin_pad (in_ch=3 first layer)
   ConvW conv(const std::string& w, const std::string& b, int cin, int cout, int ks, int cin_pad = 0) {
@@ -1680,6 +1686,7 @@ int dmx_model_destroy(dmx_model* m) {
       (void)hipGraphDestroy(m->graph);
     }
     for (void* p : m->owned) (void)hipFree(p);
+    if (m->job_tables) (void)hipFree(m->job_tables);
     if (m->ws_mem) (void)hipFree(m->ws_mem);
     if (m->tws_mem) (void)hipFree(m->tws_mem);
     if (m->bws_mem) (void)hipFree(m->bws_mem);

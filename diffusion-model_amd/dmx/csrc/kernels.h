@@ -892,10 +892,17 @@ static __global__ __launch_bounds__(256) void vae_enc_tail_kernel(const float* i
 //   kind 0: Conv2d [Cout][Cin][KS][KS], k = (ky*KS+kx)*Cin + c
 //   kind 1: Linear [Cout][Cin],        k = c
 //   kind 2: ConvTranspose2d(4,s2,p1) [Cin][Cout][4][4], phase (py,px), tap (jy,jx)
-static __global__ void repack_kernel(float* dst, const float* src, int kind, int P, int Npad, int Kpad, int Cout, int Cin,
-                              int KS) {
+struct RepackJob {
+  float* dst; const float* src; int kind, P, Npad, Kpad, Cout, Cin, KS;
+};
+struct CopyJob {
+  float* dst; const float* src; size_t n;
+};
+
+DMX_DEV void repack_range(float* dst, const float* src, int kind, int P, int Npad, int Kpad, int Cout, int Cin, int KS,
+                          size_t first, size_t stride) {
   const size_t total = (size_t)P * Npad * Kpad;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+  for (size_t i = first; i < total; i += stride) {
     const int k = (int)(i % Kpad), nn = (int)((i / Kpad) % Npad), ph = (int)(i / ((size_t)Kpad * Npad));
     float v = 0.f;
     if (kind == 0) {
@@ -915,6 +922,25 @@ static __global__ void repack_kernel(float* dst, const float* src, int kind, int
     }
     dst[i] = v;
   }
+}
+
+static __global__ void repack_kernel(float* dst, const float* src, int kind, int P, int Npad, int Kpad, int Cout, int Cin,
+                              int KS) {
+  repack_range(dst, src, kind, P, Npad, Kpad, Cout, Cin, KS, (size_t)blockIdx.x * blockDim.x + threadIdx.x,
+               (size_t)gridDim.x * blockDim.x);
+}
+
+// dmx_model_refresh: every weight repack (blockIdx.y = job) / parameter copy of the model in one
+// launch each instead of one launch per tensor (the refresh follows every optimizer step).
+static __global__ void repack_batch_kernel(const RepackJob* jobs) {
+  const RepackJob j = jobs[blockIdx.y];
+  repack_range(j.dst, j.src, j.kind, j.P, j.Npad, j.Kpad, j.Cout, j.Cin, j.KS, (size_t)blockIdx.x * blockDim.x + threadIdx.x,
+               (size_t)gridDim.x * blockDim.x);
+}
+static __global__ void copy_batch_kernel(const CopyJob* jobs) {
+  const CopyJob j = jobs[blockIdx.y];
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < j.n; i += (size_t)gridDim.x * blockDim.x)
+    j.dst[i] = j.src[i];
 }
 
 // Transpose [R][Cc] -> [Cc][R] (embedding weights for coalesced access).

@@ -819,9 +819,31 @@ static void with_fp32(dmx_model* m, F&& f) {
   m->prec = prec;
 }
 
+// Replays the packing after in-place parameter updates: all parameter copies in one launch, the
+// recorded jobs in order (padding / flip / transpose staging), then all repacks in one launch.
 static void refresh_model(dmx_model* m, hipStream_t st) {
   if (!m->finalized) throw Error(DMX_E_STATE, "model weights not finalized");
+  const size_t nc = m->copies.size(), nr = m->repacks.size();
+  if (m->job_tables_n != nc + nr) {  // (re)upload the tables (training adds repacks after finalize)
+    if (m->job_tables) HIPCHK(hipFree(m->job_tables));
+    m->job_tables = nullptr;
+    HIPCHK(hipMalloc(&m->job_tables, nc * sizeof(CopyJob) + nr * sizeof(RepackJob) + 16));
+    HIPCHK(hipMemcpy(m->job_tables, m->copies.data(), nc * sizeof(CopyJob), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(static_cast<char*>(m->job_tables) + nc * sizeof(CopyJob), m->repacks.data(),
+                     nr * sizeof(RepackJob), hipMemcpyHostToDevice));
+    m->job_tables_n = nc + nr;
+  }
+  const CopyJob* ct = static_cast<const CopyJob*>(m->job_tables);
+  const RepackJob* rt = reinterpret_cast<const RepackJob*>(static_cast<const char*>(m->job_tables) + nc * sizeof(CopyJob));
+  if (nc) {
+    copy_batch_kernel<<<dim3(4, (unsigned)nc), 256, 0, st>>>(ct);
+    HIPCHK(hipGetLastError());
+  }
   for (auto& f : m->jobs) f(st);
+  if (nr) {
+    repack_batch_kernel<<<dim3(64, (unsigned)nr), 256, 0, st>>>(rt);
+    HIPCHK(hipGetLastError());
+  }
   m->planes_stale = true;
 }
 
