@@ -52,8 +52,9 @@ class _NoisePrefetch:
     instead of preceding it.  torch.randn(shape, out=buf) consumes the generator exactly like
     torch.randn(shape)."""
 
-    def __init__(self, shape, n: int, depth: int = 2):
+    def __init__(self, shape, n: int, depth: int = 2, rows=None):
         self.shape, self.n = tuple(int(v) for v in shape), int(n)
+        self.rows = rows  # (start, end): only these rows of each draw go to the device (a rank's shard)
         self.bufs = [torch.empty(self.shape, pin_memory=True) for _ in range(depth + 2)]
         self.events = [None] * len(self.bufs)
         self.q: "queue.Queue" = queue.Queue(maxsize=depth)
@@ -78,7 +79,8 @@ class _NoisePrefetch:
         if k < 0:
             raise self.err
         j = k % len(self.bufs)
-        out = self.bufs[j].to(device, non_blocking=True)
+        src = self.bufs[j] if self.rows is None else self.bufs[j][self.rows[0]:self.rows[1]]
+        out = src.to(device, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(device))
         self.events[j] = ev

@@ -666,6 +666,11 @@ struct Run {
   Arena& ws;
   Prof* prof = nullptr;
   std::string layer;
+  // > 0: gemm() takes its tile / split-K / kernel decisions as if the batch had this many
+  // samples (the grid still covers the real batch).  The VAE decoder sets 1, so a sample's
+  // decoded bytes do not depend on the batch or chunk it is decoded in (summation order is a
+  // function of the per-sample geometry only).
+  int tile_n = 0;
   void tap(const std::string& name, const float* p, size_t count);
   void begin(const std::string& kernel, double flops, double bytes) {
     if (!prof) return;
@@ -744,16 +749,17 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
                 const float* res, float2* rowpart, int seg, const _Float16* ash = nullptr,
                 const _Float16* asl = nullptr, Deferred* defer = nullptr) {
   const int M = N * H * W;
+  const int Md = (R.tile_n > 0 ? R.tile_n : N) * H * W;  // rows the decisions below are taken for
   if (cw.cout % 32 != 0) throw Error(DMX_E_INTERNAL, "gemm: Cout must be a multiple of 32");
   const int bn = (cw.cout % 128 == 0) ? 128 : 64;
-  const int tiles128 = cdiv(M, 128) * cdiv(cw.cout, bn) * cw.phases;
+  const int tiles128 = cdiv(Md, 128) * cdiv(cw.cout, bn) * cw.phases;
   const int bm = tiles128 >= 256 ? 128 : 64;  // 128-row tiles (split K if the grid is then small) from 256 tiles
-  const int blocks = cdiv(M, bm) * cdiv(cw.cout, bn) * cw.phases;
+  const int blocks = cdiv(Md, bm) * cdiv(cw.cout, bn) * cw.phases;
   const bool x3 = R.m->prec >= 1 && src_mode == SRC_PLAIN && cw.Bh != nullptr;
   const bool x1 = x3 && R.m->prec == 2;  // config-4 fp16: one MFMA on the hi planes
   // 512-thread ping-pong kernel (256-row tiles) for the large f16-plane convs
   const bool pp = pp_enabled() && x3 && epi == EPI_STATS && cw.phases == 1 && s.C >= 32 && ash != nullptr &&
-                  (H * W) % 32 == 0 && cdiv(M, 256) * cdiv(cw.cout, bn) >= 256;  // 32-row GN partials
+                  (H * W) % 32 == 0 && cdiv(Md, 256) * cdiv(cw.cout, bn) >= 256;  // 32-row GN partials
   const int bk = pp ? 32 : x3 ? 64 : IG_BK;
   const int nkt = cw.kpad / bk;
   int splits = 1, ksplit = nkt;
@@ -1453,6 +1459,7 @@ static void validate_step(dmx_model* m, const dmx_step_args* a) {
 static void vae_body(Run& R, const float* z, float* img, uint8_t* u8, int n, int h, int w) {
   dmx_model* m = R.m;
   const int G = 8;
+  R.tile_n = 1;  // per-sample tiling decisions: decoded bytes independent of the batch / chunk
   SrcDesc s = plain_src(z, 4);
   s.C0 = 4;
   s.scale = m->cfg.scale;
@@ -1483,6 +1490,7 @@ static void vae_body(Run& R, const float* z, float* img, uint8_t* u8, int n, int
     H = Ho;
     W = Wo;
   }
+  R.tile_n = 0;
   if (R.plan) return;
   dim3 grid(cdiv(H * W, 256), n);
   R.begin("vae_tail_kernel", 2.0 * n * H * W * 3 * 576, 4.0 * (double)n * H * W * (64 + 3) + (double)n * H * W * 3);

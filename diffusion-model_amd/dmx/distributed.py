@@ -25,6 +25,11 @@ import torch
 import torch.distributed as dist
 
 
+def _diff():
+    import diff  # the drop-in sampler module (diffusion-model_amd/diff.py)
+    return diff
+
+
 def world() -> Tuple[int, int]:
     if dist.is_available() and dist.is_initialized():
         return dist.get_world_size(), dist.get_rank()
@@ -93,12 +98,25 @@ def sharded_loop(step: Callable[[torch.Tensor, int, Optional[torch.Tensor]], tor
     return x
 
 
+def any_rank(flag: bool, device) -> bool:
+    """True when `flag` is set on any rank (one tiny MAX all-reduce; the sampler's range guard)."""
+    ws, _ = world()
+    if ws == 1:
+        return bool(flag)
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32)
+    if dist.get_backend() != "gloo":
+        t = t.to(device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return bool(t.item())
+
+
 class ShardedCondSampler:
     """Multi-GPU ``sample_latent_cond``: same arguments, this rank's shard runs on its GPU,
     rank 0 receives all decoded uint8 images (HWC) or latents."""
 
     def __init__(self, diffuser, model, vae=None):
         self.d, self.model, self.vae = diffuser, model, vae
+        self.range_fallbacks = 0
 
     def sample(self, class_counts, z_shape=None, guidance_scale: float = 3.0, null_label: int = 0, cond=None,
                cond_mask=None, decode: bool = True, dummy_input_hw=(224, 224)) -> Optional[torch.Tensor]:
@@ -106,7 +124,13 @@ class ShardedCondSampler:
         (B, 8H, 8W, 3) uint8 images (decode and a VAE given) or the (B, C, H, W) latents,
         None on the other ranks.  Draw order per rank equals the single-process sampler's
         (optional encode draw, x_T, then the seed (device mode) or one global draw per step
-        (host mode)), so rank 0's result is the single-process result."""
+        (host mode)), so rank 0's result is the single-process result.
+
+        The T loop runs in Diffuser.GUARD_CHUNK pieces with the single-process sampler's
+        split-precision range guard: after each chunk every rank's range flag is OR-ed across
+        ranks (one 4-byte all-reduce per chunk) and, if any rank saw a non-finite output, EVERY
+        rank replays the chunk from its start in exact-fp32 mode (same x, same CPU-generator
+        state / Philox seed) — exactly what the single process does for the whole batch."""
         ws, rank = world()
         d = self.d
         items = d._norm_counts(class_counts)
@@ -125,7 +149,9 @@ class ShardedCondSampler:
             z_shape = d._latent_shape(self.vae, dummy_input_hw, dev)
         C, H, W = z_shape
         nm = self.model.native() if e > s else None
+        guard = d._guard_target(self.model) if nm is not None else None
         tables = d.coef_tables(dev, clamp_prev=True)
+        T = d.num_timesteps
         x = torch.randn((B, C, H, W))[s:e].to(dev).contiguous()  # x_T (diff.py:327), global draw
         if d.noise_source == "device":
             seed = torch.tensor([d._seed()], dtype=torch.long)  # drawn after x_T, as _run_cond_loop does
@@ -133,20 +159,52 @@ class ShardedCondSampler:
                 if dist.get_backend() != "gloo":
                     seed = seed.to(dev)
                 dist.broadcast(seed, src=0)
-            if e > s:
-                t_dev = torch.full((1,), d.num_timesteps, dtype=torch.long, device=dev)
-                nm.sample_loop(x, t_dev, y, null_label, v, m, float(guidance_scale), tables, d.num_timesteps,
-                               seed=int(seed.item()), sample_offset=s, use_graph=d.use_graph)
+            seed = int(seed.item())
+            t_dev = torch.full((1,), T, dtype=torch.long, device=dev)
+
+            def run(i_from, i_to, xs):  # device Philox loop, graph-replayed, t decremented in-graph
+                if xs.shape[0] > 0:
+                    t_dev.fill_(i_from)
+                    nm.sample_loop(xs, t_dev, y, null_label, v, m, float(guidance_scale), tables, i_from - i_to,
+                                   seed=seed, sample_offset=s, use_graph=d.use_graph)
+                return xs
         else:
-            def step(xs, t, noise):
-                if xs.shape[0] == 0:  # empty shard (B < world size): nothing to compute
-                    return xs
-                out = torch.empty_like(xs)
-                tt = torch.full((xs.shape[0],), t, dtype=torch.long, device=dev)
-                nm.step(xs, out, tt, y, null_label, v, m, float(guidance_scale), tables, noise)
-                return out
-            for i in range(d.num_timesteps, 0, -1):
-                x = step(x, i, host_noise_slice((B, C, H, W), s, e, dev))
+            def run(i_from, i_to, xs):
+                """One global CPU-generator draw per step (this shard's rows kept), made one step
+                ahead on a helper thread into pinned buffers (diff._NoisePrefetch: same generator,
+                same order), so the host draw of the global tensor overlaps the GPU step."""
+                pf = _diff()._NoisePrefetch((B, C, H, W), i_from - i_to, rows=(s, e)) if dev.type == "cuda" else None
+                try:
+                    for i in range(i_from, i_to, -1):
+                        noise = pf.next(dev) if pf is not None else host_noise_slice((B, C, H, W), s, e, dev)
+                        if xs.shape[0] > 0:  # an empty shard (B < world size) only keeps the draw order
+                            out = torch.empty_like(xs)
+                            tt = torch.full((xs.shape[0],), i, dtype=torch.long, device=dev)
+                            nm.step(xs, out, tt, y, null_label, v, m, float(guidance_scale), tables, noise)
+                            xs = out
+                finally:
+                    if pf is not None:
+                        pf.close()
+                return xs
+
+        with torch.no_grad():
+            i = T
+            while i >= 1:
+                j = max(i - d.GUARD_CHUNK, 0)
+                x0, rng = x.clone(), torch.get_rng_state()
+                x = run(i, j, x)
+                tripped = guard.range_tripped() if guard is not None else False
+                if any_rank(tripped, dev):
+                    torch.set_rng_state(rng)
+                    x = x0
+                    if guard is not None:
+                        with guard.precision_override("fp32"):
+                            x = run(i, j, x)
+                        guard.range_tripped()  # clear
+                    else:
+                        x = run(i, j, x)
+                    self.range_fallbacks += 1
+                i = j
         if decode and self.vae is not None:
             if e > s:
                 _, u8 = self.vae.native().decode(x, want_img=False, want_u8=True)

@@ -170,6 +170,90 @@ def test_sharded_sampler_world2_equals_single_process(fn):
     assert torch.equal(res[0], single)
 
 
+class _GuardNative(_FakeNative):
+    """A stub native model with the split-precision range guard: in "x3" mode a step on a class-3
+    sample raises the range flag and adds a visible error; "fp32" mode is exact.  Only the rank
+    holding the class-3 samples trips, so both ranks must replay (the sharded sampler
+    runs the single-process guard)."""
+
+    def __init__(self):
+        self.precision = "x3"
+        self.flag = False
+
+    def _mark(self, xs, y):
+        if self.precision == "x3":
+            xs.add_(1e-3)  # the split-precision error every x3 step carries (absent in fp32 mode)
+            if bool((y == 3).any()):
+                self.flag = True
+                xs.add_(0.25)
+
+    def step(self, xs, out, tt, y, null_label, v, m, g, tables, noise):
+        super().step(xs, out, tt, y, null_label, v, m, g, tables, noise)
+        self._mark(out, y)
+
+    def sample_loop(self, x, t_dev, y, null_label, v, m, g, tables, steps, seed=0, sample_offset=0, use_graph=True):
+        super().sample_loop(x, t_dev, y, null_label, v, m, g, tables, steps, seed, sample_offset, use_graph)
+        self._mark(x, y)
+
+    def range_tripped(self, reset=True):
+        f = self.flag
+        if reset:
+            self.flag = False
+        return f
+
+    def precision_override(self, prec):
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            old, self.precision = self.precision, prec
+            try:
+                yield self
+            finally:
+                self.precision = old
+        return cm()
+
+
+class _GuardModel:
+    _dmx_kind = 2  # looks like a dmx UnetCondWithGeomHead to diff._native_kind
+
+    def __init__(self):
+        self._n = _GuardNative()
+
+    def native(self):
+        return self._n
+
+
+def _guarded(rank, world, mode):
+    import diff
+    d = diff.Diffuser(4, device="cpu")
+    d.noise_source = mode
+    torch.manual_seed(7)
+    s = dd.ShardedCondSampler(d, _GuardModel(), None)
+    out = s.sample({1: 3, 3: 2}, z_shape=(2, 3, 3), decode=False)
+    return None if out is None else (out.clone(), s.range_fallbacks)
+
+
+def _guarded_host(rank, world):
+    return _guarded(rank, world, "host")
+
+
+def _guarded_device(rank, world):
+    return _guarded(rank, world, "device")
+
+
+@pytest.mark.parametrize("fn", [_guarded_host, _guarded_device])
+def test_sharded_sampler_range_guard_replays_on_every_rank(fn):
+    """A range trip on rank 1 only makes every rank replay the chunk in fp32: rank 0's gathered
+    latents equal the single-process guarded run, and carry no x3 error."""
+    res = run(fn)
+    single, nfall = fn(0, 1)
+    assert nfall == 1 and res[1] is None
+    out, nf0 = res[0]
+    assert nf0 == 1
+    assert torch.equal(out, single)
+
+
 def test_gather_rows_rejects_wrong_shard():
     res = run(_bad_gather)
     assert res[0] == "ValueError" and res[1] == "ValueError"

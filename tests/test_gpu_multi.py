@@ -82,12 +82,11 @@ def test_sharded_sampler_world2_on_one_gpu(cuda, mode):
     single = _job(mode, decode=True)
     assert res[1] is None and res[0].shape == single.shape == (5, 128, 128, 3)
     d = np.abs(res[0].numpy().astype(np.int32) - single.numpy().astype(np.int32))
-    # Usually <= 1.2e-5 of the values at +-1.  About one run in three of this one-GPU two-rank
-    # rehearsal (both ranks' kernels interleaved on one device) has shown +-1 on up to 3 % of
-    # the pixels, while the sharded latents were bit-identical to the single-process ones in
-    # every diagnostic repeat (tools/diag_multi.py, tools/diag_decode.py) — open issue, see
-    # DESIGN.md §7.  The latent contract stays strict in test_sharded_sampler_latents_world2_host.
-    assert d.max() <= 1 and (d > 0).mean() <= 5e-2, (int(d.max()), float((d > 0).mean()))
+    # The decoder takes its tiling / split-K decisions per sample (engine.hip vae_body, Run::tile_n),
+    # so a sample's bytes do not depend on the shard it is decoded in (test_gpu_parity.py
+    # test_vae_decode_batch_invariant); the U-Net step's decisions still follow the shard's batch
+    # size, so latents may differ in summation order only.  Pixel contract of every other test.
+    assert d.max() <= 1 and (d > 0).mean() <= 1e-3, (int(d.max()), float((d > 0).mean()))
 
 
 def test_sharded_sampler_latents_world2_host(cuda):
@@ -117,6 +116,44 @@ def test_sharded_world1_equals_diffuser_device_mode(cuda):
     ref_lat = d.sample_latent_cond(m, {1: 3, 3: 2}, z_shape=(4, 16, 16), vae=None, progress=False, cond=vals,
                                    cond_mask=mask)
     assert torch.equal(lat, ref_lat.cpu())
+
+
+def test_sharded_world1_range_guard_equals_diffuser(cuda, unet_sd_overflow):
+    """the sharded sampler runs the split-precision range guard.  An overflowing GroupNorm
+    gamma trips it; world 1 must replay the chunk in fp32 exactly as Diffuser.sample_latent_cond."""
+    import diff
+    from dmx import distributed as dd
+    from models.unet_cond_geom import UnetCondWithGeomHead
+    dev = torch.device("cuda:0")
+    outs = []
+    for sharded in (True, False):
+        m = UnetCondWithGeomHead()
+        m.load_state_dict(unet_sd_overflow)
+        m.to(dev).eval()
+        d = diff.Diffuser(4, device=dev)
+        g = torch.Generator().manual_seed(35)
+        vals = torch.rand((2, 12), generator=g).to(dev)
+        mask = torch.ones((2, 12), device=dev)
+        torch.manual_seed(36)
+        if sharded:
+            s = dd.ShardedCondSampler(d, m, None)
+            lat = s.sample({1: 1, 2: 1}, z_shape=(4, 16, 16), cond=vals, cond_mask=mask, decode=False)
+            assert s.range_fallbacks == 1
+        else:
+            lat = d.sample_latent_cond(m, {1: 1, 2: 1}, z_shape=(4, 16, 16), vae=None, progress=False, cond=vals,
+                                       cond_mask=mask)
+            assert d.range_fallbacks == 1
+        assert torch.isfinite(lat).all() and m.native().precision == "x3"
+        outs.append(lat.cpu())
+    assert torch.equal(outs[0], outs[1])
+
+
+@pytest.fixture
+def unet_sd_overflow():
+    from dmx import synth
+    sd = synth.unet_cond_geom_weights(0)
+    sd["inc.double_conv.1.weight"] = sd["inc.double_conv.1.weight"] * 1e5
+    return sd
 
 
 # ---- data-parallel training step (SURVEY.md §8f rank 2) ----------------------------------

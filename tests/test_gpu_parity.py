@@ -166,6 +166,29 @@ def test_vae_decode_vs_oracle_odd_batch(vae, cuda, vae_sd):
     assert rel(img, exp) < TOL
 
 
+@pytest.mark.parametrize("hw", [16, 32])
+@pytest.mark.parametrize("vprec", ["x3", "fp32"])
+def test_vae_decode_batch_invariant(vae, cuda, hw, vprec):
+    """a latent's decoded image does not depend on the batch it is decoded in —
+    the same 5 latents decoded as n=5, as n=3 + n=2 and one by one give identical fp32 images and
+    uint8 bytes (the decoder's tile / split-K decisions are per sample; diff.py:353 decodes in
+    chunks of 4, the sharded sampler in shards of any size)."""
+    nat = vae.native()
+    z = torch.randn((5, 4, hw, hw), generator=torch.Generator().manual_seed(6)).to(cuda)
+
+    def dec(zz):
+        img, u8 = nat.decode(zz.contiguous(), want_img=True, want_u8=True)
+        return img.cpu(), u8.cpu()
+
+    with nat.precision_override(vprec):
+        full = dec(z)
+        parts = [dec(z[:3]), dec(z[3:])]
+        ones = [dec(z[i:i + 1]) for i in range(5)]
+    for split in (parts, ones):
+        assert torch.equal(torch.cat([p[0] for p in split]), full[0])
+        assert torch.equal(torch.cat([p[1] for p in split]), full[1])
+
+
 def test_denoise_cond_golden_steps(golden, model, cuda):
     import diff
     g = golden("denoise_cond.npz")
