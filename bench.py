@@ -56,6 +56,10 @@ def parse():
                     help="steps timed for the fp32-MFMA and host-noise legs beside the headline (0 = skip)")
     ap.add_argument("--train-steps", type=int, default=10, help="training-step leg (0 = skip)")
     ap.add_argument("--train-batch", type=int, default=32)
+    ap.add_argument("--no-e2e", dest="e2e", action="store_false",
+                    help="skip the end-to-end config-2 sample (T steps + decode + uint8 + PIL) leg")
+    ap.add_argument("--sharded-T", type=int, default=50,
+                    help="steps of the ShardedCondSampler leg (config 3 path incl. decode + gather; 0 = skip)")
     ap.add_argument("--png-steps", type=int, default=100,
                     help="steps of the generate_steps drop-in (async PNG pipeline) timed for config 5 (0 = skip)")
     return ap.parse_args()
@@ -359,6 +363,129 @@ def roofline(records, pmc=None):
     return rl, agg
 
 
+def lib_sha256() -> str:
+    import hashlib
+    from dmx import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def load_pmc():
+    """PMC HBM bytes per launch (profiles/pmc_traffic.json, tools/pmc_traffic.py) — only when that
+    file was measured on THIS library build (its lib_sha256 equals the loaded libdmx.so's);
+    otherwise `traffic` stays null and the note says why."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None, "no profiles/pmc_traffic.json"
+    doc = json.load(open(path))
+    have, want = doc.get("lib_sha256"), lib_sha256()
+    if have != want:
+        return None, f"stale: profiles/pmc_traffic.json is of build {str(have)[:12]}, loaded build {want[:12]}"
+    return doc.get("traffic_bytes_per_launch"), f"profiles/pmc_traffic.json (build {want[:12]})"
+
+
+def e2e_sample(model, args, dev):
+    """One full BASELINE config-2 sample end to end (reference diff.py:326-369 as the drop-in runs it):
+    Diffuser.sample_latent_cond with device (Philox) noise — x_T draw, the T-step CFG loop (graph
+    replay, range-guarded chunks), empty_cache, the VAE decode of all B latents (uint8 HWC on the
+    device), the D2H copy and the PIL conversion — as wall seconds.  The decode + D2H + PIL tail is
+    also timed alone."""
+    import diff
+    from dmx import synth
+    from models.vae import VAE
+    vae = VAE()
+    vae.load_state_dict(synth.vae_weights(1))
+    vae = vae.to(dev).eval()
+    _, y, vals, mask = make_inputs(args.batch, args.hw, dev, seed=11)
+    counts = [(c, int((y == c).sum())) for c in (1, 2, 3)]
+    order = torch.argsort(y, stable=True)  # the sampler lays out classes in count order
+    vals, mask = vals[order].contiguous(), mask[order].contiguous()
+    kw = dict(z_shape=(4, args.hw, args.hw), vae=vae, to_pil=True, progress=False, cond=vals, cond_mask=mask)
+    warm = diff.Diffuser(diff.Diffuser.GUARD_CHUNK, device=dev)
+    warm.noise_source = "device"
+    warm.sample_latent_cond(model, counts, **kw)  # graph capture, decode workspace
+    d = diff.Diffuser(args.T, device=dev)
+    d.noise_source = "device"
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    imgs = d.sample_latent_cond(model, counts, **kw)
+    dt = time.perf_counter() - t0
+    assert len(imgs) == args.batch and imgs[0].size == (8 * args.hw, 8 * args.hw)
+    z = torch.randn((args.batch, 4, args.hw, args.hw), generator=torch.Generator().manual_seed(3)).to(dev)
+    d._decode(vae, z, True)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    d._decode(vae, z, True)
+    tail = time.perf_counter() - t1
+    return {"workload": f"config 2 end to end: one sample_latent_cond call, B={args.batch}, T={args.T}, CFG "
+                        f"{args.guidance}, device noise, VAE decode to {8 * args.hw}x{8 * args.hw} uint8 + PIL",
+            "seconds": round(dt, 4), "images_per_s": round(args.batch / dt, 2),
+            "loop_steps_per_s": round(args.T / max(dt - tail, 1e-9), 2),
+            "decode_d2h_pil_ms": round(tail * 1e3, 2), "range_fallbacks": d.range_fallbacks}
+
+
+def sharded_sample(model, args, dev, world, rank):
+    """BASELINE config 3 path (multi-GPU): dmx.distributed.ShardedCondSampler.sample over a global batch
+    of B x world (B per rank), device noise, a T_s-step CFG loop, per-rank VAE decode and the C2
+    gather of all uint8 images on rank 0 (dist.gather; RCCL under torchrun).  Reports the whole call
+    (max over ranks) and the gather alone."""
+    import diff
+    from dmx import distributed as dd
+    from dmx import synth
+    from models.vae import VAE
+    vae = VAE()
+    vae.load_state_dict(synth.vae_weights(1))
+    vae = vae.to(dev).eval()
+    Bg = args.batch * world
+    T = args.sharded_T
+    counts = [(1, Bg - 2 * (Bg // 3)), (2, Bg // 3), (3, Bg // 3)]
+
+    def run():
+        d = diff.Diffuser(T, device=dev)
+        d.noise_source = "device"
+        torch.manual_seed(21)
+        return dd.ShardedCondSampler(d, model, vae).sample(counts, z_shape=(4, args.hw, args.hw),
+                                                            guidance_scale=args.guidance, decode=True)
+
+    def synced():
+        torch.cuda.synchronize()
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    def max_over_ranks(v):
+        if world == 1:
+            return v
+        import torch.distributed as dist
+        e = torch.tensor([v], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        return float(e.item())
+
+    run()
+    synced()
+    t0 = time.perf_counter()
+    imgs = run()
+    synced()
+    dt = max_over_ranks(time.perf_counter() - t0)
+    if rank == 0:
+        assert imgs is not None and imgs.shape == (Bg, 8 * args.hw, 8 * args.hw, 3)
+    s, e = dd.shard_range(Bg, world, rank)
+    u8 = torch.zeros((e - s, 8 * args.hw, 8 * args.hw, 3), dtype=torch.uint8, device=dev)
+    dd.gather_rows(u8, Bg)
+    synced()
+    t1 = time.perf_counter()
+    dd.gather_rows(u8, Bg)
+    synced()
+    g = max_over_ranks(time.perf_counter() - t1)
+    return {"workload": f"config 3 path: ShardedCondSampler.sample, global B={Bg} ({args.batch} per rank), T={T}, "
+                        f"device noise, per-rank decode, uint8 gather to rank 0",
+            "seconds": round(dt, 4), "steps_per_s": round(T / dt, 2),
+            "job_batch_steps_per_s": round(world * T / dt, 2),
+            "images_per_s": round(Bg / dt, 2), "gather_ms": round(g * 1e3, 3),
+            "gather_bytes": Bg * 64 * args.hw * args.hw * 3, "n_gpus": world,
+            "backend": (__import__("torch.distributed").distributed.get_backend() if world > 1 else "none")}
+
+
 def config5(nm, args, tables, seed):
     """BASELINE config 5 (generate_steps.py:158-187): B=1, and before every denoise_cond the
     current latent x_t is decoded by the frozen VAE to a 256x256 uint8 image (the PNG write
@@ -524,6 +651,10 @@ def main():
         out["config5"] = config5(nm, args, tables, seed)
     if world == 1 and args.legs_steps > 0:
         out.update(legs(nm, model, x, y, vals, mask, args, tables, seed))
+    if world == 1 and args.e2e:
+        out["e2e"] = e2e_sample(model, args, dev)
+    if args.sharded_T > 0:
+        out["sharded_sample"] = sharded_sample(model, args, dev, world, rank)
     if args.train_steps > 0:
         out["train_step"] = train_leg(args, dev, world, rank)
     if rank == 0:
@@ -532,11 +663,9 @@ def main():
             tp = torch.full((args.batch,), args.T, dtype=torch.long, device=dev)
             nm.step_profile(xp, xp, tp, y, 0, vals, mask, args.guidance, tables, None, seed=seed)  # warm
             recs = nm.step_profile(xp, xp, tp, y, 0, vals, mask, args.guidance, tables, None, seed=seed)
-            pmc = None
-            pmc_path = os.path.join(REPO, "profiles", "pmc_traffic.json")
-            if os.path.exists(pmc_path):
-                pmc = json.load(open(pmc_path)).get("traffic_bytes_per_launch")
+            pmc, pmc_note = load_pmc()
             rl, agg = roofline(recs, pmc)
+            rl["traffic_source"] = pmc_note
             out["roofline"] = rl
             if os.environ.get("DMX_BENCH_BREAKDOWN"):
                 with open(os.environ["DMX_BENCH_BREAKDOWN"], "w") as f:

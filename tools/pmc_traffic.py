@@ -28,6 +28,15 @@ def load(d, counter):
     return vals
 
 
+def lib_sha256():
+    """Build identity of the profiled library (bench.py refuses PMC bytes of another build)."""
+    import hashlib
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "diffusion-model_amd"))
+    from dmx import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def main(fetch_dir, write_dir, out):
     fe, wr = load(fetch_dir, "FETCH_SIZE"), load(write_dir, "WRITE_SIZE")
     res = {}
@@ -40,6 +49,7 @@ def main(fetch_dir, write_dir, out):
                      "--steps 3 --warmup 1 --cpu-steps 0 --config4-steps 0 --config5-steps 0 --no-profile` (tools/prof.sh); bytes/launch = 2*FETCH_SIZE*1024 + "
                      "WRITE_SIZE*1024 (gfx950 FETCH_SIZE = half of wide coalesced reads); averages over all "
                      "launches of the kernel name",
+           "lib_sha256": lib_sha256(),
            "traffic_bytes_per_launch": {k: round(v["bytes"]) for k, v in res.items()},
            "detail": res}
     json.dump(doc, open(out, "w"), indent=1)

@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-r02}
 OUT=gpurun_out/profiles
 mkdir -p $OUT
-ARGS="--steps 10 --warmup 2 --cpu-steps 0 --config4-steps 0 --config5-steps 0 --legs-steps 0 --png-steps 0 --train-steps 0"
+ARGS="--steps 10 --warmup 2 --cpu-steps 0 --config4-steps 0 --config5-steps 0 --legs-steps 0 --png-steps 0 --train-steps 0 --no-e2e --sharded-T 0"
 PMC_ARGS="$ARGS --no-profile"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/prof_trace.log 2>&1
 cp "$(find gpurun_out/prof_trace -name '*kernel_stats.csv' | head -1)" $OUT/${TAG}_kernel_stats.csv
