@@ -19,6 +19,7 @@
 #include "kernels.h"
 #include "igemm_pp.h"
 #include "launch.h"
+#include "igemm_halo.h"
 #include "tokmlp.h"
 #include "eval.h"
 #include "train.h"
@@ -179,6 +180,8 @@ struct ConvW {
   float* B = nullptr;           // fp32 [phases][npad][kpad]
   _Float16* Bh = nullptr;       // split-precision planes (scaled by 1/inv_scale)
   _Float16* Bl = nullptr;
+  _Float16* Fh = nullptr;       // the planes again in MFMA-fragment order (3x3 convs read by the
+  _Float16* Fl = nullptr;       // halo kernel straight into registers; igemm_halo.h frag_planes_kernel)
   float inv_scale = 1.f;
   float* bias = nullptr;
   int cin = 0, cout = 0, taps = 0, kpad = 0, npad = 0, phases = 1;
@@ -336,6 +339,12 @@ static void split_planes(ConvW& c, hipStream_t st, unsigned* slot) {
   c.inv_scale = std::ldexp(1.0f, -e);
   split_weights_kernel<<<(int)std::min<size_t>((n + 255) / 256, 8192), 256, 0, st>>>(c.B, c.Bh, c.Bl, n, scale);
   HIPCHK(hipGetLastError());
+  if (c.Fh != nullptr) {
+    const size_t chunks = n / 8;
+    frag_planes_kernel<<<(int)std::min<size_t>((chunks + 255) / 256, 8192), 256, 0, st>>>(c.Bh, c.Bl, c.Fh, c.Fl,
+                                                                                          c.npad, c.kpad);
+    HIPCHK(hipGetLastError());
+  }
 }
 
 // Every split-GEMM weight of the model (the f16 planes are re-derived after a refresh).
@@ -406,6 +415,15 @@ struct Packer {
     m->owned.push_back(l);
     c.Bh = static_cast<_Float16*>(h);
     c.Bl = static_cast<_Float16*>(l);
+    if (c.taps == 9 && c.phases == 1 && c.cout % 64 == 0 && c.cin % 32 == 0 && c.kpad == 9 * c.cin) {
+      // halo-kernel candidate (gemm(): 3x3, Cout % 64, whole 32-channel chunks)
+      HIPCHK(hipMalloc(&h, n * sizeof(_Float16)));
+      m->owned.push_back(h);
+      HIPCHK(hipMalloc(&l, n * sizeof(_Float16)));
+      m->owned.push_back(l);
+      c.Fh = static_cast<_Float16*>(h);
+      c.Fl = static_cast<_Float16*>(l);
+    }
     split_planes(c, st, absmax_slot());
   }
   unsigned* absmax_slot() {
@@ -700,6 +718,19 @@ static bool cat_planes_enabled() { return true; }
 // two-block kernel, same-box A/B).
 static bool pp_enabled() { return true; }
 
+// The halo-staged 3x3 conv (igemm_halo.h) for the large 16x16 / 32x32 convs.  DMX_HALO (same-box
+// A/B): 2 (default) B staged in LDS per step — measured +2.4 … +2.7 % per CFG step over the
+// ping-pong / register-staged kernels it replaces; 1 B read straight into registers (fragment-
+// ordered planes, one barrier per chunk) — at parity with the old kernels; 0 off.
+static int halo_mode() {
+  static const int v = [] {
+    const char* e = std::getenv("DMX_HALO");
+    return e == nullptr ? 2 : std::atoi(e);
+  }();
+  return v;
+}
+static bool halo_enabled() { return halo_mode() != 0; }
+
 // Implicit GEMM: conv3x3 (taps 9), ConvT phases (taps 4, phases 4), conv4x4-s2 (taps 16),
 // linear (taps 1).  Sources are plain NHWC (or the NCHW network input); grids too small to
 // fill the 256 CUs are split along K into deterministic slabs reduced by splitk_reduce_kernel
@@ -760,10 +791,19 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   // 512-thread ping-pong kernel (256-row tiles) for the large f16-plane convs
   const bool pp = pp_enabled() && x3 && epi == EPI_STATS && cw.phases == 1 && s.C >= 32 && ash != nullptr &&
                   (H * W) % 32 == 0 && cdiv(Md, 256) * cdiv(cw.cout, bn) >= 256;  // 32-row GN partials
+  // halo-staged 3x3 conv (igemm_halo.h): 256-pixel tiles of whole image rows (W = 16 / 32), the
+  // chunk's input halo staged once for all nine taps; where it fills >= 256 blocks without split-K
+  int hbn = 0;
+  if (halo_enabled() && x3 && epi == EPI_STATS && cw.phases == 1 && cw.taps == 9 && (W == 16 || W == 32) &&
+      (H * W) % 256 == 0 && s.C % 32 == 0 && cw.kpad == 9 * s.C && cw.Fh != nullptr &&
+      (ash != nullptr || src_mode == SRC_PLAIN)) {
+    if (cw.cout % 128 == 0 && (Md / 256) * (cw.cout / 128) >= 256) hbn = 128;
+    else if (cw.cout % 64 == 0 && (Md / 256) * (cw.cout / 64) >= 256) hbn = 64;
+  }
   const int bk = pp ? 32 : x3 ? 64 : IG_BK;
   const int nkt = cw.kpad / bk;
   int splits = 1, ksplit = nkt;
-  if (!pp && cw.phases == 1 && blocks < 512 && nkt * bk >= 512) {  // split K below 2 blocks / CU
+  if (!hbn && !pp && cw.phases == 1 && blocks < 512 && nkt * bk >= 512) {  // split K below 2 blocks / CU
     splits = std::min(std::min(8, std::max(2, 512 / blocks)), nkt * bk / 256);
     ksplit = cdiv(nkt, splits);
     splits = cdiv(nkt, ksplit);
@@ -828,6 +868,8 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   xp.Bh = cw.Bh;
   xp.Bl = cw.Bl;
   xp.inv_scale = cw.inv_scale;
+  xp.Fh = cw.Fh;
+  xp.Fl = cw.Fl;
   {
     const size_t a_el = (size_t)N * p.Hin * p.Win * s.C;
     const size_t ab = a_el * (ash != nullptr ? 2 : 4), bb = (size_t)cw.npad * cw.kpad * 2;
@@ -863,6 +905,15 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
     const int rb = cdiv(M * (cw.cout / 4), 256);
     R.begin("splitk_reduce_kernel", 0.0, 4.0 * (double)(splits + 1) * M * cw.cout);
     splitk_reduce_kernel<<<rb, 256, 0, R.st>>>(q);
+    R.end();
+    HIPCHK(hipGetLastError());
+    return rrows;
+  }
+  if (hbn) {  // halo-staged 3x3 conv, 256-pixel x hbn tiles (igemm_halo.h)
+    dim3 gh(M / 256, cw.cout / hbn, 1);
+    std::snprintf(nm, sizeof nm, "igemm_halo_kernel<%d, %d, %d, %d, %d>", hbn, (int)EPI_STATS, sa, x1 ? 1 : 0, W);
+    R.begin(nm, flops, bytes);
+    launch_halo(halo_mode(), hbn, W, sa, x1 ? 1 : 0, xp, gh, R.st);
     R.end();
     HIPCHK(hipGetLastError());
     return rrows;

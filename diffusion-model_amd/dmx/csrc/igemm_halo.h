@@ -1,0 +1,465 @@
+// dmx — split-precision 3x3 convolution with the input halo staged once per channel chunk
+// ("halo conv"), gfx950.
+//
+// Same arithmetic as igemm_x3_kernel (igemm_x3.h): fp32 operands as fp16 hi + lo, three
+// v_mfma_f32_32x32x16_f16 per product (al*bh, ah*bl, ah*bh), fp32 accumulate, weights pre-split
+// and pre-scaled.  What differs is how A reaches LDS.  The implicit GEMMs stage A per K-tile =
+// (tap, channel slice), so every input pixel is loaded, (split,) and written to LDS nine times.
+// Here a 512-thread block owns 256 output pixels (TR whole image rows of one sample, W = 16 or
+// 32) x BN output channels and walks K as (32-channel chunk) x (9 taps): the chunk's input halo
+// — (TR + 2) x (W + 2) pixels, zero outside the image — is staged ONCE as f16 hi / lo planes, and
+// the nine taps read their A fragments from it at a per-tap pixel offset (row r of a fragment is
+// output pixel (y, x) of the tile; tap (dy, dx) reads halo pixel (y + 1 + dy, x + 1 + dx)).
+// A staging falls from 9 to (TR + 2)(W + 2) / (TR W) = 1.33 (W = 32) / 1.27 (W = 16) loads per
+// input element; only the B (weight) slice is staged per step.
+//
+// K order (sum order of every output element): chunk-major, taps 0..8 inside a chunk, k16 steps
+// inside a tap — a fixed function of (C, tap geometry), independent of the grid.
+//
+// Schedule: one barrier per (chunk, tap) step.  Step s computes from A buffer (chunk & 1) and B
+// buffer (s & 1); the B slice of step s + 1 is loaded into registers at the start of step s and
+// written to B buffer (s + 1) & 1 after the step's MFMAs (that buffer's readers, step s - 1, passed
+// the barrier ending step s - 1); the next chunk's halo is loaded at the chunk's tap 0 and written
+// to the other A buffer after tap 1 (its readers, the previous chunk, finished before tap 0).
+// LDS (80-byte rows, conflict-free ds_read_b128 as in igemm_x3): A 2 x HP x 40 f16 x 2 planes
+// (108.8 KB at W = 32), B 2 x BN x 40 f16 x 2 planes (41 KB at BN = 128): one block per CU, two
+// waves per SIMD.  Waves: 4 (rows) x 2 (columns), 64 x BN/2 each.
+#pragma once
+#include "common.h"
+#include "igemm.h"
+#include "igemm_x3.h"
+
+namespace dmx {
+
+template <int BN, int EPI, int SA, int X1, int W>
+__global__ __launch_bounds__(512) void igemm_halo_kernel(const X3Params P) {
+  const IgemmParams& p = P.g;
+  constexpr int TR = 256 / W;                     // output image rows per tile
+  constexpr int HWD = W + 2, HP = (TR + 2) * HWD;  // halo row width / pixels
+  constexpr int CK = 32, RS = CK + 8;              // channels per chunk, f16 per LDS row
+  constexpr int WN = BN / 2, TM = 2, TN = WN / 32;
+  constexpr int PW = SA ? 8 : 4;                   // channels per staged A piece (16 bytes)
+  constexpr int PPR = CK / PW;                     // pieces per halo pixel per plane
+  constexpr int NPI = (HP * PPR + 511) / 512;      // halo pieces per thread
+  constexpr int BCH = BN * (CK / 8);               // B chunks (16 bytes) per plane per step
+  static_assert(TN >= 1 && BCH <= 512, "tile");
+
+  constexpr int LA = X1 ? 1 : HP, LB = X1 ? 1 : BN;
+  __shared__ __attribute__((aligned(16))) _Float16 Ah[2][HP][RS];
+  __shared__ __attribute__((aligned(16))) _Float16 Al[2][LA][RS];
+  __shared__ __attribute__((aligned(16))) _Float16 Bhs[2][BN][RS];
+  __shared__ __attribute__((aligned(16))) _Float16 Bls[2][LB][RS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  int mt, nt, bz;
+  xcd_tile(mt, nt, bz);
+  const int m0 = mt * 256, n0 = nt * BN;
+  const int HW = p.H * W;
+  const int C = p.src.C;
+  const int nsmp = m0 / HW, y0 = (m0 - nsmp * HW) / W;  // tile = rows y0 .. y0 + TR - 1 of sample nsmp
+  constexpr int AES = SA ? 2 : 4;
+
+  // halo pieces of this thread: element offset of channel 0 of the piece (chunk 0), or -1 (zero)
+  int hoff[NPI];
+  short hpix[NPI], hq[NPI];
+#pragma unroll
+  for (int i = 0; i < NPI; ++i) {
+    const int e = tid + 512 * i;
+    const int h = e / PPR, q = e - h * PPR;
+    hpix[i] = (short)h;
+    hq[i] = (short)q;
+    const int hy = h / HWD, hx = h - hy * HWD;
+    const int y = y0 + hy - 1, x = hx - 1;
+    const bool ok = e < HP * PPR && y >= 0 && y < p.H && x >= 0 && x < W;
+    hoff[i] = ok ? (((nsmp * p.H + y) * W + x) * C + q * PW) : -1;
+  }
+  const __amdgpu_buffer_rsrc_t rAh = rsrc_of(SA ? (const void*)P.Ash : (const void*)p.src.src0, P.a_bytes);
+  const __amdgpu_buffer_rsrc_t rAl = rsrc_of(SA ? (const void*)P.Asl : (const void*)p.src.src0, P.a_bytes);
+  const __amdgpu_buffer_rsrc_t rBh = rsrc_of(P.Bh, P.b_bytes), rBl = rsrc_of(P.Bl, P.b_bytes);
+  const bool bact = tid < BCH;
+  const int brow = tid / (CK / 8), bq = tid - brow * (CK / 8);
+  const int boffs = ((n0 + brow) * p.Kpad + bq * 8) * 2;
+
+  // register stages
+  floatx4 ha4[SA ? 1 : NPI];
+  half8 hah[SA ? NPI : 1], hal[SA ? NPI : 1];
+  half8 rbh, rbl;
+  auto load_halo = [&](int c) {
+#pragma unroll
+    for (int i = 0; i < NPI; ++i) {
+      const int off = hoff[i] >= 0 ? (hoff[i] + c * CK) * AES : kOOB;
+      if constexpr (SA) {
+        hah[i] = bload_h8(rAh, off, 0);
+        if constexpr (!X1) hal[i] = bload_h8(rAl, off, 0);
+      } else {
+        ha4[i] = bload_f4(rAh, off, 0);
+      }
+    }
+  };
+  auto store_halo = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < NPI; ++i) {
+      if (tid + 512 * i >= HP * PPR) continue;  // only the last piece index can be partial
+      const int h = hpix[i], q = hq[i];
+      if constexpr (SA) {
+        *reinterpret_cast<half8*>(&Ah[buf][h][q * 8]) = hah[i];
+        if constexpr (!X1) *reinterpret_cast<half8*>(&Al[buf][h][q * 8]) = hal[i];
+      } else if constexpr (X1) {
+        *reinterpret_cast<half4*>(&Ah[buf][h][q * 4]) = __builtin_convertvector(ha4[i], half4);
+      } else {
+        half4 hh, ll;
+        split4(ha4[i], hh, ll);
+        *reinterpret_cast<half4*>(&Ah[buf][h][q * 4]) = hh;
+        *reinterpret_cast<half4*>(&Al[buf][h][q * 4]) = ll;
+      }
+    }
+  };
+  // B slice of step (chunk c, tap t): k = t * C + c * CK .. + CK of the [Npad][Kpad] planes
+  auto load_b = [&](int c, int t) {
+    if (bact) {
+      const int soff = (t * C + c * CK) * 2;
+      rbh = bload_h8(rBh, boffs, soff);
+      if constexpr (!X1) rbl = bload_h8(rBl, boffs, soff);
+    }
+  };
+  auto store_b = [&](int buf) {
+    if (bact) {
+      *reinterpret_cast<half8*>(&Bhs[buf][brow][bq * 8]) = rbh;
+      if constexpr (!X1) *reinterpret_cast<half8*>(&Bls[buf][brow][bq * 8]) = rbl;
+    }
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int fr = lane & 31, fh = lane >> 5;
+  // halo pixel of each A fragment row for tap (0, 0): output pixel r = wm*64 + i*32 + fr of the tile
+  int abase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = wm * 64 + i * 32 + fr;
+    const int ly = r / W, lx = r - ly * W;
+    abase[i] = (ly + 1) * HWD + lx + 1;
+  }
+  auto compute = [&](int abuf, int bbuf, int tap) {
+    const int ty = (tap * 11) >> 5;  // tap / 3 for tap in [0, 8]
+    const int delta = (ty - 1) * HWD + (tap - 3 * ty - 1);
+    constexpr int S = CK / 16, NR = (X1 ? 1 : 2) * (TM + TN), NM = (X1 ? 1 : 3) * TM * TN;
+    half8 ah[2][TM], al[2][TM], bh[2][TN], bl[2][TN];
+    auto ldf = [&](int s, int d) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = abase[i] + delta;
+        ah[d][i] = *reinterpret_cast<const half8*>(&Ah[abuf][row][16 * s + 8 * fh]);
+        if constexpr (!X1) al[d][i] = *reinterpret_cast<const half8*>(&Al[abuf][row][16 * s + 8 * fh]);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WN + j * 32 + fr;
+        bh[d][j] = *reinterpret_cast<const half8*>(&Bhs[bbuf][row][16 * s + 8 * fh]);
+        if constexpr (!X1) bl[d][j] = *reinterpret_cast<const half8*>(&Bls[bbuf][row][16 * s + 8 * fh]);
+      }
+    };
+    ldf(0, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      const int d = s & 1;
+      if (s + 1 < S) ldf(s + 1, d ^ 1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (!X1) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[d][i], bh[d][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[d][i], bl[d][j], acc[i][j], 0, 0, 0);
+          }
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[d][i], bh[d][j], acc[i][j], 0, 0, 0);
+        }
+      if (s + 1 < S) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, NM - NR, 0);
+      } else {
+        __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
+      }
+    }
+  };
+
+  const int nch = C / CK;
+  const int S = nch * 9;
+  // prologue: chunk 0's halo and step 0's B slice
+  load_b(0, 0);
+  load_halo(0);
+  store_b(0);
+  store_halo(0);
+  __syncthreads();
+  int c = 0, t = 0;
+  for (int s = 0; s < S; ++s) {
+    // next step's (chunk, tap)
+    const int c1 = t == 8 ? c + 1 : c, t1 = t == 8 ? 0 : t + 1;
+    if (s + 1 < S) load_b(c1, t1);
+    if (t == 0 && c + 1 < nch) load_halo(c + 1);
+    compute(c & 1, s & 1, t);
+    if (t == 1 && c + 1 < nch) store_halo((c + 1) & 1);
+    if (s + 1 < S) store_b((s + 1) & 1);
+    __syncthreads();
+    c = c1;
+    t = t1;
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] *= P.inv_scale;
+
+  // rows of wave (wm, wn): m0 + wm * 64 + ...; the shared epilogue's 2 x 2 wave grid over 128 rows
+  igemm_epilogue<128, BN, EPI>(p, acc, 0, m0 + (wm >> 1) * 128, n0, wm & 1, wn, fr, fh);
+}
+
+
+// The split weight planes ([Npad][Kpad] f16) re-laid out in MFMA-fragment order: the B operand of
+// v_mfma_f32_32x32x16_f16 for columns 32*nb .. +31 and k = 16*kk .. +15 is 64 lanes x 8 f16, lane
+// (fr, fh) holding column 32*nb + fr, k = 16*kk + 8*fh .. +7 — stored as 1 KB contiguous at
+// ((nb * Kpad/16 + kk) * 64 + lane) * 8, so a wave loads a fragment with one coalesced 16-byte-per-
+// lane load.  Replayed after every plane refresh (engine.hip split_planes).
+static __global__ void frag_planes_kernel(const _Float16* bh, const _Float16* bl, _Float16* fh, _Float16* fl,
+                                          int npad, int kpad) {
+  const size_t chunks = (size_t)npad * kpad / 8;
+  const int kc8 = kpad / 8;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < chunks; i += (size_t)gridDim.x * blockDim.x) {
+    const int n = (int)(i / kc8), kc = (int)(i - (size_t)n * kc8);
+    const int nb = n >> 5, fr = n & 31, kk = kc >> 1, hh = kc & 1;
+    const size_t dst = ((size_t)(nb * (kpad / 16) + kk) * 64 + hh * 32 + fr) * 8;
+    *reinterpret_cast<half8*>(fh + dst) = *reinterpret_cast<const half8*>(bh + i * 8);
+    *reinterpret_cast<half8*>(fl + dst) = *reinterpret_cast<const half8*>(bl + i * 8);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Halo conv with B read straight into registers ("B-direct").  The A halo is staged as above;
+// every wave loads its own B fragments for the NEXT (chunk, tap) step from the fragment-ordered
+// planes (P.Fh / P.Fl: one coalesced 1 KB load per fragment, L2-resident weights; the four waves
+// of a column group read the same bytes, mostly L1 hits) while the current step's MFMAs run, so
+// B never touches LDS and the only barrier is the one per 32-channel chunk (halo buffer swap):
+// MFMAs flow across the nine taps of a chunk.  A fragments are read one k16 step ahead, across
+// tap boundaries too.  Same K order as igemm_halo_kernel.
+// ---------------------------------------------------------------------------
+template <int BN, int EPI, int SA, int X1, int W>
+__global__ __launch_bounds__(512) void igemm_halo_bd_kernel(const X3Params P) {
+  const IgemmParams& p = P.g;
+  constexpr int TR = 256 / W;
+  constexpr int HWD = W + 2, HP = (TR + 2) * HWD;
+  constexpr int CK = 32, RS = CK + 8;
+  constexpr int WN = BN / 2, TM = 2, TN = WN / 32;
+  constexpr int PW = SA ? 8 : 4;
+  constexpr int PPR = CK / PW;
+  constexpr int NPI = (HP * PPR + 511) / 512;
+  constexpr int NP = X1 ? 1 : 2;  // B planes
+  static_assert(TN >= 1, "tile");
+
+  constexpr int LA = X1 ? 1 : HP;
+  __shared__ __attribute__((aligned(16))) _Float16 Ah[2][HP][RS];
+  __shared__ __attribute__((aligned(16))) _Float16 Al[2][LA][RS];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  int mt, nt, bz;
+  xcd_tile(mt, nt, bz);
+  const int m0 = mt * 256, n0 = nt * BN;
+  const int HW = p.H * W;
+  const int C = p.src.C;
+  const int nsmp = m0 / HW, y0 = (m0 - nsmp * HW) / W;
+  constexpr int AES = SA ? 2 : 4;
+
+  // halo pieces of this thread (index e = tid + 512 i): element offset of channel 0 (chunk 0) or -1
+  int hoff[NPI];
+#pragma unroll
+  for (int i = 0; i < NPI; ++i) {
+    const int e = tid + 512 * i;
+    const int h = e / PPR, q = e - h * PPR;
+    const int hy = h / HWD, hx = h - hy * HWD;
+    const int y = y0 + hy - 1, x = hx - 1;
+    const bool ok = e < HP * PPR && y >= 0 && y < p.H && x >= 0 && x < W;
+    hoff[i] = ok ? (((nsmp * p.H + y) * W + x) * C + q * PW) : -1;
+  }
+  const __amdgpu_buffer_rsrc_t rAh = rsrc_of(SA ? (const void*)P.Ash : (const void*)p.src.src0, P.a_bytes);
+  const __amdgpu_buffer_rsrc_t rAl = rsrc_of(SA ? (const void*)P.Asl : (const void*)p.src.src0, P.a_bytes);
+  const __amdgpu_buffer_rsrc_t rFh = rsrc_of(P.Fh, P.b_bytes), rFl = rsrc_of(P.Fl, P.b_bytes);
+
+  // The next chunk's halo is staged in HR rounds of PR pieces per thread (round r: loaded at tap 2r,
+  // written at tap 2r + 1) so only PR pieces are held in registers at a time.
+  constexpr int HR = 4, PR = (NPI + HR - 1) / HR;
+  floatx4 ha4[SA ? 1 : PR];
+  half8 hah[SA ? PR : 1], hal[SA ? PR : 1];
+  auto load_halo = [&](int c, int r) {
+#pragma unroll
+    for (int k = 0; k < PR; ++k) {
+      const int i = r * PR + k;
+      if (i >= NPI) break;
+      const int off = hoff[i] >= 0 ? (hoff[i] + c * CK) * AES : kOOB;
+      if constexpr (SA) {
+        hah[k] = bload_h8(rAh, off, 0);
+        if constexpr (!X1) hal[k] = bload_h8(rAl, off, 0);
+      } else {
+        ha4[k] = bload_f4(rAh, off, 0);
+      }
+    }
+  };
+  auto store_halo = [&](int buf, int r) {
+#pragma unroll
+    for (int k = 0; k < PR; ++k) {
+      const int i = r * PR + k;
+      if (i >= NPI) break;
+      const int e = tid + 512 * i;
+      if (e >= HP * PPR) continue;
+      const int h = e / PPR, q = e - h * PPR;
+      if constexpr (SA) {
+        *reinterpret_cast<half8*>(&Ah[buf][h][q * 8]) = hah[k];
+        if constexpr (!X1) *reinterpret_cast<half8*>(&Al[buf][h][q * 8]) = hal[k];
+      } else if constexpr (X1) {
+        *reinterpret_cast<half4*>(&Ah[buf][h][q * 4]) = __builtin_convertvector(ha4[k], half4);
+      } else {
+        half4 hh, ll;
+        split4(ha4[k], hh, ll);
+        *reinterpret_cast<half4*>(&Ah[buf][h][q * 4]) = hh;
+        *reinterpret_cast<half4*>(&Al[buf][h][q * 4]) = ll;
+      }
+    }
+  };
+  // B fragments of one step: [column tile j][k16 step s][plane]
+  struct BF {
+    half8 v[TN][2][NP];
+  };
+  const int kk16 = p.Kpad / 16;
+  const int voff = lane * 16;
+  auto load_bf = [&](int c, int t, BF& b) {
+    const int kk = (t * C + c * CK) / 16;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int nb = (n0 + wn * WN + j * 32) >> 5;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int soff = (nb * kk16 + kk + s) * 1024;
+        b.v[j][s][0] = bload_h8(rFh, voff, soff);
+        if constexpr (!X1) b.v[j][s][1] = bload_h8(rFl, voff, soff);
+      }
+    }
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int fr = lane & 31, fh = lane >> 5;
+  int abase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int r = wm * 64 + i * 32 + fr;
+    const int ly = r / W, lx = r - ly * W;
+    abase[i] = (ly + 1) * HWD + lx + 1;
+  }
+  auto tap_delta = [&](int tap) {
+    const int ty = (tap * 11) >> 5;
+    return (ty - 1) * HWD + (tap - 3 * ty - 1);
+  };
+  // A fragments, two k16 slots
+  half8 ah[2][TM], al[2][TM];
+  auto lda = [&](int abuf, int tap, int s, int d) {
+    const int delta = tap_delta(tap);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = abase[i] + delta;
+      ah[d][i] = *reinterpret_cast<const half8*>(&Ah[abuf][row][16 * s + 8 * fh]);
+      if constexpr (!X1) al[d][i] = *reinterpret_cast<const half8*>(&Al[abuf][row][16 * s + 8 * fh]);
+    }
+  };
+  auto mfmas = [&](int d, const BF& b, int s) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (!X1) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[d][i], b.v[j][s][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[d][i], b.v[j][s][1], acc[i][j], 0, 0, 0);
+        }
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[d][i], b.v[j][s][0], acc[i][j], 0, 0, 0);
+      }
+  };
+  constexpr int NRA = (X1 ? 1 : 2) * TM, NM = (X1 ? 1 : 3) * TM * TN;
+
+  const int nch = C / CK;
+  const int S = nch * 9;
+  BF b0, b1;
+  load_bf(0, 0, b0);
+#pragma unroll
+  for (int r = 0; r < HR; ++r) {
+    load_halo(0, r);
+    store_halo(0, r);
+  }
+  __syncthreads();
+  lda(0, 0, 0, 0);
+  // one (chunk, tap) step: MFMAs from A buffer c & 1 and `cur`; loads the next step's B into `nxt`
+  auto step = [&](int s, BF& cur, BF& nxt) {
+    const int c = s / 9, t = s - c * 9;
+    const int abuf = c & 1;
+    if (s + 1 < S) load_bf(t == 8 ? c + 1 : c, t == 8 ? 0 : t + 1, nxt);
+    if ((t & 1) == 0 && t < 2 * HR && c + 1 < nch) load_halo(c + 1, t >> 1);
+    lda(abuf, t, 1, 1);  // k16 step 1 of this tap, under step 0's MFMAs
+    mfmas(0, cur, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+#pragma unroll
+    for (int r = 0; r < NRA; ++r) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, NM - NRA - 1, 0);
+    if (t < 8) {
+      lda(abuf, t + 1, 0, 0);  // next tap's k16 step 0, under step 1's MFMAs
+      mfmas(1, cur, 1);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+#pragma unroll
+      for (int r = 0; r < NRA; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, NM - NRA - 1, 0);
+    } else {
+      mfmas(1, cur, 1);
+    }
+    if ((t & 1) == 1 && t < 2 * HR && c + 1 < nch) store_halo((c + 1) & 1, t >> 1);
+    if (t == 8 && s + 1 < S) {
+      __syncthreads();  // chunk c + 1's halo complete in buffer (c + 1) & 1; buffer c & 1 free
+      lda((c + 1) & 1, 0, 0, 0);
+    }
+  };
+  for (int s = 0; s < S; s += 2) {
+    step(s, b0, b1);
+    if (s + 1 < S) step(s + 1, b1, b0);
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] *= P.inv_scale;
+
+  igemm_epilogue<128, BN, EPI>(p, acc, 0, m0 + (wm >> 1) * 128, n0, wm & 1, wn, fr, fh);
+}
+
+}  // namespace dmx

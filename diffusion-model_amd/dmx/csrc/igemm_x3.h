@@ -38,6 +38,8 @@ struct X3Params {
   float inv_scale;         // 2^-e
   unsigned a_bytes;        // bytes of the A source (one plane) — buffer-load range
   unsigned b_bytes;        // bytes of one phase of one B plane ([Npad][Kpad] f16)
+  const _Float16* Fh;      // the B planes in MFMA-fragment order (igemm_halo.h), or null
+  const _Float16* Fl;
 };
 
 
