@@ -730,6 +730,13 @@ static int halo_mode() {
   return v;
 }
 static bool halo_enabled() { return halo_mode() != 0; }
+static bool gn_fuse_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("DMX_GN_FUSE");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return v;
+}
 
 // Implicit GEMM: conv3x3 (taps 9), ConvT phases (taps 4, phases 4), conv4x4-s2 (taps 16),
 // linear (taps 1).  Sources are plain NHWC (or the NCHW network input); grids too small to
@@ -776,9 +783,32 @@ static void check_range(Run& R, const void* p, size_t bytes, const char* what) {
   throw Error(DMX_E_INTERNAL, msg);
 }
 
+// GroupNorm(1, C) + GELU applied by the halo conv while it stages its raw fp32 source (the
+// ResBlock's mid normalisation, igemm_halo.h GNA).
+struct GnLoad {
+  const float2* rowpart = nullptr;  // [N][cnt] partials of the producing conv
+  int cnt = 0;
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+};
+
+// Output-channel tile of the halo-staged 3x3 conv for this GEMM, or 0 when it does not apply
+// (igemm_halo.h: 256-pixel tiles of whole rows of one sample, W = 16 / 32, 32-channel chunks,
+// >= 256 blocks without split-K, EPI_STATS).
+static int halo_bn(const Run& R, int src_C, int N, int H, int W, const ConvW& cw, int epi, bool plain_or_planes) {
+  const int Md = (R.tile_n > 0 ? R.tile_n : N) * H * W;
+  const bool x3 = R.m->prec >= 1 && cw.Bh != nullptr;
+  if (!(halo_enabled() && x3 && epi == EPI_STATS && cw.phases == 1 && cw.taps == 9 && (W == 16 || W == 32) &&
+        (H * W) % 256 == 0 && src_C % 32 == 0 && cw.kpad == 9 * src_C && cw.Fh != nullptr && plain_or_planes))
+    return 0;
+  if (cw.cout % 128 == 0 && (Md / 256) * (cw.cout / 128) >= 256) return 128;
+  if (cw.cout % 64 == 0 && (Md / 256) * (cw.cout / 64) >= 256) return 64;
+  return 0;
+}
+
 static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, const ConvW& cw, int epi, float* out,
                 const float* res, float2* rowpart, int seg, const _Float16* ash = nullptr,
-                const _Float16* asl = nullptr, Deferred* defer = nullptr) {
+                const _Float16* asl = nullptr, Deferred* defer = nullptr, const GnLoad* gn = nullptr) {
   const int M = N * H * W;
   const int Md = (R.tile_n > 0 ? R.tile_n : N) * H * W;  // rows the decisions below are taken for
   if (cw.cout % 32 != 0) throw Error(DMX_E_INTERNAL, "gemm: Cout must be a multiple of 32");
@@ -793,13 +823,9 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
                   (H * W) % 32 == 0 && cdiv(Md, 256) * cdiv(cw.cout, bn) >= 256;  // 32-row GN partials
   // halo-staged 3x3 conv (igemm_halo.h): 256-pixel tiles of whole image rows (W = 16 / 32), the
   // chunk's input halo staged once for all nine taps; where it fills >= 256 blocks without split-K
-  int hbn = 0;
-  if (halo_enabled() && x3 && epi == EPI_STATS && cw.phases == 1 && cw.taps == 9 && (W == 16 || W == 32) &&
-      (H * W) % 256 == 0 && s.C % 32 == 0 && cw.kpad == 9 * s.C && cw.Fh != nullptr &&
-      (ash != nullptr || src_mode == SRC_PLAIN)) {
-    if (cw.cout % 128 == 0 && (Md / 256) * (cw.cout / 128) >= 256) hbn = 128;
-    else if (cw.cout % 64 == 0 && (Md / 256) * (cw.cout / 64) >= 256) hbn = 64;
-  }
+  const int hbn = halo_bn(R, s.C, N, H, W, cw, epi, ash != nullptr || src_mode == SRC_PLAIN);
+  if (gn != nullptr && (hbn == 0 || ash != nullptr || src_mode != SRC_PLAIN))
+    throw Error(DMX_E_INTERNAL, "gemm: GroupNorm-on-load needs the halo conv on a plain fp32 source");
   const int bk = pp ? 32 : x3 ? 64 : IG_BK;
   const int nkt = cw.kpad / bk;
   int splits = 1, ksplit = nkt;
@@ -870,6 +896,9 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   xp.inv_scale = cw.inv_scale;
   xp.Fh = cw.Fh;
   xp.Fl = cw.Fl;
+  xp.gn_rowpart = nullptr;
+  xp.gn_cnt = 0;
+  xp.gn_gamma = xp.gn_beta = nullptr;
   {
     const size_t a_el = (size_t)N * p.Hin * p.Win * s.C;
     const size_t ab = a_el * (ash != nullptr ? 2 : 4), bb = (size_t)cw.npad * cw.kpad * 2;
@@ -911,9 +940,17 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   }
   if (hbn) {  // halo-staged 3x3 conv, 256-pixel x hbn tiles (igemm_halo.h)
     dim3 gh(M / 256, cw.cout / hbn, 1);
-    std::snprintf(nm, sizeof nm, "igemm_halo_kernel<%d, %d, %d, %d, %d>", hbn, (int)EPI_STATS, sa, x1 ? 1 : 0, W);
+    const int gna = gn != nullptr ? 1 : 0;
+    if (gna) {
+      xp.gn_rowpart = gn->rowpart;
+      xp.gn_cnt = gn->cnt;
+      xp.gn_gamma = gn->gamma;
+      xp.gn_beta = gn->beta;
+    }
+    std::snprintf(nm, sizeof nm, "igemm_halo_kernel<%d, %d, %d, %d, %d, %d>", hbn, (int)EPI_STATS, sa, x1 ? 1 : 0, W,
+                  gna);
     R.begin(nm, flops, bytes);
-    launch_halo(halo_mode(), hbn, W, sa, x1 ? 1 : 0, xp, gh, R.st);
+    launch_halo(gna ? 2 : halo_mode(), hbn, W, sa, x1 ? 1 : 0, gna, xp, gh, R.st);
     R.end();
     HIPCHK(hipGetLastError());
     return rrows;
@@ -1058,10 +1095,26 @@ static float* resblock(Run& R, const ResW& w, const SrcDesc& in, int mode, int N
     n1.out_h = a1h;
     n1.out_l = a1l;
   }
-  if (d1.fused) reduce_norm(R, d1, n1, N);
-  else norm(R, n1, N);
-  const int rr2 = gemm(R, plain_src(a1, w.mid), SRC_PLAIN, N, H, W, w.c2, EPI_STATS, r2, nullptr, rp2, seg,
-                       planes ? a1h : nullptr, planes ? a1l : nullptr, &d2);
+  // The mid GroupNorm + GELU folded into conv2's halo staging (igemm_halo.h GNA) where conv2 runs
+  // the halo conv and conv1 wrote whole-sample partials (no split-K slabs): no norm_kernel launch,
+  // no hi / lo planes.  DMX_GN_FUSE=0 turns it off (the staged operand is the same either way).
+  const bool fuse1 = gn_fuse_enabled() && planes && !d1.fused && !R.m->debug &&
+                     halo_bn(R, w.mid, N, H, W, w.c2, EPI_STATS, true) > 0;
+  int rr2;
+  if (fuse1) {
+    GnLoad g;
+    g.rowpart = rp1;
+    g.cnt = rr1 * (w.mid / seg);
+    g.gamma = w.g1.p;
+    g.beta = w.b1.p;
+    rr2 = gemm(R, plain_src(r1, w.mid), SRC_PLAIN, N, H, W, w.c2, EPI_STATS, r2, nullptr, rp2, seg, nullptr, nullptr,
+               &d2, &g);
+  } else {
+    if (d1.fused) reduce_norm(R, d1, n1, N);
+    else norm(R, n1, N);
+    rr2 = gemm(R, plain_src(a1, w.mid), SRC_PLAIN, N, H, W, w.c2, EPI_STATS, r2, nullptr, rp2, seg,
+               planes ? a1h : nullptr, planes ? a1l : nullptr, &d2);
+  }
   NormParams n2 = norm_params(r2, rp2, w.cout / seg, rr2, w.g2.p, w.b2.p, w.cout, HW, out);
   if (residual) {
     if (mode != SRC_PLAIN) throw Error(DMX_E_INTERNAL, "residual ResBlock needs a plain input");

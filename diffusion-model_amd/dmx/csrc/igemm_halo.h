@@ -31,7 +31,12 @@
 
 namespace dmx {
 
-template <int BN, int EPI, int SA, int X1, int W>
+// GNA = 1: the source is a raw conv output (fp32, SA = 0) whose GroupNorm(1, C) + GELU is applied
+// while the halo is staged (P.gn_*: the producing conv's (sum, sum of squares) partials of each
+// sample, gamma, beta) — the ResBlock's mid norm_kernel launch and its hi / lo planes disappear.
+// Statistics are reduced exactly as norm_kernel reduces them and the affine + GELU is the same
+// expression, so the staged operand is bit-identical to the planes norm_kernel would have written.
+template <int BN, int EPI, int SA, int X1, int W, int GNA = 0>
 __global__ __launch_bounds__(512) void igemm_halo_kernel(const X3Params P) {
   const IgemmParams& p = P.g;
   constexpr int TR = 256 / W;                     // output image rows per tile
@@ -81,10 +86,46 @@ __global__ __launch_bounds__(512) void igemm_halo_kernel(const X3Params P) {
   const int brow = tid / (CK / 8), bq = tid - brow * (CK / 8);
   const int boffs = ((n0 + brow) * p.Kpad + bq * 8) * 2;
 
-  // register stages
+  static_assert(!GNA || !SA, "GroupNorm-on-load reads the fp32 raw source");
+  // GroupNorm(1, C) statistics of sample nsmp, reduced as norm_kernel does (threads 0..255 sum
+  // strided partials in double, wave shuffle tree, ((w0 + w1) + (w2 + w3)))
+  float2 gst = make_float2(0.f, 0.f);
+  if constexpr (GNA) {
+    __shared__ double gr1[4], gr2[4];
+    __shared__ float2 gst_s;
+    if (tid < 256) {
+      const float2* rp = P.gn_rowpart + (size_t)nsmp * P.gn_cnt;
+      double s1 = 0.0, s2 = 0.0;
+      for (int i = tid; i < P.gn_cnt; i += 256) {
+        const float2 q = rp[i];
+        s1 += (double)q.x;
+        s2 += (double)q.y;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        s1 += __shfl_xor(s1, o, 64);
+        s2 += __shfl_xor(s2, o, 64);
+      }
+      if ((tid & 63) == 0) {
+        gr1[tid >> 6] = s1;
+        gr2[tid >> 6] = s2;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const double cntd = (double)HW * (double)C;
+      const double mean = ((gr1[0] + gr1[1]) + (gr1[2] + gr1[3])) / cntd;
+      double var = ((gr2[0] + gr2[1]) + (gr2[2] + gr2[3])) / cntd - mean * mean;
+      var = var < 0.0 ? 0.0 : var;
+      gst_s = make_float2((float)mean, (float)(1.0 / sqrt(var + 1e-5)));
+    }
+    __syncthreads();
+    gst = gst_s;
+  }
+  // register stages (B: two sets, a step's slice is loaded two steps before it is read)
   floatx4 ha4[SA ? 1 : NPI];
   half8 hah[SA ? NPI : 1], hal[SA ? NPI : 1];
-  half8 rbh, rbl;
+  half8 rbh[2], rbl[2];
   auto load_halo = [&](int c) {
 #pragma unroll
     for (int i = 0; i < NPI; ++i) {
@@ -97,36 +138,49 @@ __global__ __launch_bounds__(512) void igemm_halo_kernel(const X3Params P) {
       }
     }
   };
-  auto store_halo = [&](int buf) {
+  // pieces [i0, i1) of the staged halo to LDS buffer `buf` (chunk cc)
+  auto store_halo = [&](int buf, int cc, int i0, int i1) __attribute__((always_inline)) {
+    const int cst = cc * CK;  // first channel of the chunk (GroupNorm affine)
+    (void)cst;
 #pragma unroll
     for (int i = 0; i < NPI; ++i) {
+      if (i < i0 || i >= i1) continue;
       if (tid + 512 * i >= HP * PPR) continue;  // only the last piece index can be partial
       const int h = hpix[i], q = hq[i];
       if constexpr (SA) {
         *reinterpret_cast<half8*>(&Ah[buf][h][q * 8]) = hah[i];
         if constexpr (!X1) *reinterpret_cast<half8*>(&Al[buf][h][q * 8]) = hal[i];
-      } else if constexpr (X1) {
-        *reinterpret_cast<half4*>(&Ah[buf][h][q * 4]) = __builtin_convertvector(ha4[i], half4);
       } else {
-        half4 hh, ll;
-        split4(ha4[i], hh, ll);
-        *reinterpret_cast<half4*>(&Ah[buf][h][q * 4]) = hh;
-        *reinterpret_cast<half4*>(&Al[buf][h][q * 4]) = ll;
+        floatx4 v = ha4[i];
+        if constexpr (GNA) {  // GroupNorm + GELU of the raw source; zero padding stays zero
+          const int ch = cst + q * 4;
+          v = gn_apply4v(v, gst, ld4(P.gn_gamma + ch), ld4(P.gn_beta + ch), 1);
+          if (hoff[i] < 0) v = floatx4{0.f, 0.f, 0.f, 0.f};
+        }
+        if constexpr (X1) {
+          *reinterpret_cast<half4*>(&Ah[buf][h][q * 4]) = __builtin_convertvector(v, half4);
+        } else {
+          half4 hh, ll;
+          split4(v, hh, ll);
+          *reinterpret_cast<half4*>(&Ah[buf][h][q * 4]) = hh;
+          *reinterpret_cast<half4*>(&Al[buf][h][q * 4]) = ll;
+        }
       }
     }
   };
-  // B slice of step (chunk c, tap t): k = t * C + c * CK .. + CK of the [Npad][Kpad] planes
-  auto load_b = [&](int c, int t) {
+  // B slice of step s = 9 c + t: k = t * C + c * CK .. + CK of the [Npad][Kpad] planes
+  auto load_b = [&](int s, int set) {
     if (bact) {
+      const int c = s / 9, t = s - 9 * c;
       const int soff = (t * C + c * CK) * 2;
-      rbh = bload_h8(rBh, boffs, soff);
-      if constexpr (!X1) rbl = bload_h8(rBl, boffs, soff);
+      rbh[set] = bload_h8(rBh, boffs, soff);
+      if constexpr (!X1) rbl[set] = bload_h8(rBl, boffs, soff);
     }
   };
-  auto store_b = [&](int buf) {
+  auto store_b = [&](int buf, int set) {
     if (bact) {
-      *reinterpret_cast<half8*>(&Bhs[buf][brow][bq * 8]) = rbh;
-      if constexpr (!X1) *reinterpret_cast<half8*>(&Bls[buf][brow][bq * 8]) = rbl;
+      *reinterpret_cast<half8*>(&Bhs[buf][brow][bq * 8]) = rbh[set];
+      if constexpr (!X1) *reinterpret_cast<half8*>(&Bls[buf][brow][bq * 8]) = rbl[set];
     }
   };
 
@@ -197,24 +251,31 @@ __global__ __launch_bounds__(512) void igemm_halo_kernel(const X3Params P) {
 
   const int nch = C / CK;
   const int S = nch * 9;
-  // prologue: chunk 0's halo and step 0's B slice
+  // The B slice of step s is loaded at the start of step s - 2 (register set s & 1) and written to
+  // LDS after the MFMAs of step s - 1; the next chunk's halo is loaded at tap 0 and written after
+  // tap HST — the global loads get two (B) / HST + 1 (halo) steps of MFMAs to land.
+  // The halo is written in NRD rounds at taps HST .. HST + NRD - 1 (PRD pieces each), which spreads
+  // the GroupNorm + GELU VALU work of GNA over several steps' MFMAs.
+  constexpr int HST = 4, NRD = 4, PRD = (NPI + NRD - 1) / NRD;
+  // prologue: chunk 0's halo and step 0's B slice in LDS, step 1's B slice in flight
   load_b(0, 0);
   load_halo(0);
-  store_b(0);
-  store_halo(0);
+  store_b(0, 0);
+  store_halo(0, 0, 0, NPI);
+  if (S > 1) load_b(1, 1);
   __syncthreads();
-  int c = 0, t = 0;
-  for (int s = 0; s < S; ++s) {
-    // next step's (chunk, tap)
-    const int c1 = t == 8 ? c + 1 : c, t1 = t == 8 ? 0 : t + 1;
-    if (s + 1 < S) load_b(c1, t1);
+  auto step = [&](int s, int set) {  // set = (s + 1) & 1: holds B(s + 1); B(s + 2) goes to the other
+    const int c = s / 9, t = s - 9 * c;
+    if (s + 2 < S) load_b(s + 2, set ^ 1);
     if (t == 0 && c + 1 < nch) load_halo(c + 1);
     compute(c & 1, s & 1, t);
-    if (t == 1 && c + 1 < nch) store_halo((c + 1) & 1);
-    if (s + 1 < S) store_b((s + 1) & 1);
+    if (t >= HST && t < HST + NRD && c + 1 < nch) store_halo((c + 1) & 1, c + 1, (t - HST) * PRD, (t - HST + 1) * PRD);
+    if (s + 1 < S) store_b((s + 1) & 1, set);
     __syncthreads();
-    c = c1;
-    t = t1;
+  };
+  for (int s = 0; s < S; s += 2) {
+    step(s, 1);
+    if (s + 1 < S) step(s + 1, 0);
   }
 #pragma unroll
   for (int i = 0; i < TM; ++i)

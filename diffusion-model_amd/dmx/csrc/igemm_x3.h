@@ -40,6 +40,11 @@ struct X3Params {
   unsigned b_bytes;        // bytes of one phase of one B plane ([Npad][Kpad] f16)
   const _Float16* Fh;      // the B planes in MFMA-fragment order (igemm_halo.h), or null
   const _Float16* Fl;
+  // GroupNorm(1, C) + GELU applied to the raw fp32 source while staging (igemm_halo.h GNA):
+  const float2* gn_rowpart;  // [N][gn_cnt] (sum, sum of squares) partials of the producing conv
+  int gn_cnt;
+  const float* gn_gamma;
+  const float* gn_beta;
 };
 
 

@@ -1,27 +1,34 @@
-// dmx — igemm_halo_kernel (halo-staged split-precision 3x3 conv) instantiations (see launch.h).
+// dmx — igemm_halo_kernel / igemm_halo_bd_kernel (halo-staged split-precision 3x3 conv)
+// instantiations (see launch.h).
 #include "igemm_halo.h"
 #include "launch.h"
 
 namespace dmx {
 
 template <int BN, int SA, int X1, int W>
-static void go(int mode, const X3Params& p, dim3 grid, hipStream_t st) {
+static void go(int mode, int gna, const X3Params& p, dim3 grid, hipStream_t st) {
+  if constexpr (SA == 0) {
+    if (gna) {
+      igemm_halo_kernel<BN, EPI_STATS, 0, X1, W, 1><<<grid, 512, 0, st>>>(p);
+      return;
+    }
+  }
   if (mode == 2) igemm_halo_kernel<BN, EPI_STATS, SA, X1, W><<<grid, 512, 0, st>>>(p);
   else igemm_halo_bd_kernel<BN, EPI_STATS, SA, X1, W><<<grid, 512, 0, st>>>(p);
 }
 
 template <int SA, int X1>
-static void by_shape(int mode, int bn, int w, const X3Params& p, dim3 grid, hipStream_t st) {
+static void by_shape(int mode, int bn, int w, int gna, const X3Params& p, dim3 grid, hipStream_t st) {
   if (w == 32) {
-    if (bn == 128) go<128, SA, X1, 32>(mode, p, grid, st); else go<64, SA, X1, 32>(mode, p, grid, st);
+    if (bn == 128) go<128, SA, X1, 32>(mode, gna, p, grid, st); else go<64, SA, X1, 32>(mode, gna, p, grid, st);
   } else {
-    if (bn == 128) go<128, SA, X1, 16>(mode, p, grid, st); else go<64, SA, X1, 16>(mode, p, grid, st);
+    if (bn == 128) go<128, SA, X1, 16>(mode, gna, p, grid, st); else go<64, SA, X1, 16>(mode, gna, p, grid, st);
   }
 }
 
-void launch_halo(int mode, int bn, int w, int sa, int x1, const X3Params& p, dim3 grid, hipStream_t st) {
-  if (sa) { if (x1) by_shape<1, 1>(mode, bn, w, p, grid, st); else by_shape<1, 0>(mode, bn, w, p, grid, st); }
-  else { if (x1) by_shape<0, 1>(mode, bn, w, p, grid, st); else by_shape<0, 0>(mode, bn, w, p, grid, st); }
+void launch_halo(int mode, int bn, int w, int sa, int x1, int gna, const X3Params& p, dim3 grid, hipStream_t st) {
+  if (sa) { if (x1) by_shape<1, 1>(mode, bn, w, 0, p, grid, st); else by_shape<1, 0>(mode, bn, w, 0, p, grid, st); }
+  else { if (x1) by_shape<0, 1>(mode, bn, w, gna, p, grid, st); else by_shape<0, 0>(mode, bn, w, gna, p, grid, st); }
 }
 
 }  // namespace dmx

@@ -21,7 +21,8 @@ void launch_pp(int bn, int sa, int x1, const X3Params& p, dim3 grid, hipStream_t
 // width w in {16, 32}; k_halo.hip.
 // mode 1: B fragments read straight from the fragment-ordered planes into registers (one barrier
 // per channel chunk); mode 2: B staged in LDS per step (one barrier per step).
-void launch_halo(int mode, int bn, int w, int sa, int x1, const X3Params& p, dim3 grid, hipStream_t st);
+// gna = 1 (mode 2, sa = 0): GroupNorm + GELU of the raw source applied while staging.
+void launch_halo(int mode, int bn, int w, int sa, int x1, int gna, const X3Params& p, dim3 grid, hipStream_t st);
 // exact-fp32 MFMA implicit GEMM (igemm.h), k_f32.hip.
 void launch_f32(int src_mode, int epi, int bm, int bn, const IgemmParams& p, dim3 grid, hipStream_t st);
 // attention cores (k_attn.hip): split-precision (D, waves-per-EU hint, x1) and exact fp32 (D, QT).
