@@ -719,13 +719,15 @@ static bool cat_planes_enabled() { return true; }
 static bool pp_enabled() { return true; }
 
 // The halo-staged 3x3 conv (igemm_halo.h) for the large 16x16 / 32x32 convs.  DMX_HALO (same-box
-// A/B): 2 (default) B staged in LDS per step — measured +2.4 … +2.7 % per CFG step over the
-// ping-pong / register-staged kernels it replaces; 1 B read straight into registers (fragment-
-// ordered planes, one barrier per chunk) — at parity with the old kernels; 0 off.
+// A/B): 4 (default) B staged in LDS per step, 16-wave blocks (4 x 4 waves of 64 x 32 at BN = 128,
+// 8 x 2 of 32 x 32 at BN = 64) — +2.1 % per CFG step over 2; 2: the same with 8-wave blocks
+// (4 x 2 waves) — +2.4 … +2.7 % over the ping-pong / register-staged kernels it replaced; 5: BN =
+// 128 as 8 x 2 waves of 32 x 64 (between 2 and 4); 1: B read straight into registers (fragment-
+// ordered planes, one barrier per chunk) — at parity with the old kernels; 0: off.
 static int halo_mode() {
   static const int v = [] {
     const char* e = std::getenv("DMX_HALO");
-    return e == nullptr ? 2 : std::atoi(e);
+    return e == nullptr ? 4 : std::atoi(e);
   }();
   return v;
 }
@@ -950,7 +952,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
     std::snprintf(nm, sizeof nm, "igemm_halo_kernel<%d, %d, %d, %d, %d, %d>", hbn, (int)EPI_STATS, sa, x1 ? 1 : 0, W,
                   gna);
     R.begin(nm, flops, bytes);
-    launch_halo(gna ? 2 : halo_mode(), hbn, W, sa, x1 ? 1 : 0, gna, xp, gh, R.st);
+    launch_halo(halo_mode(), hbn, W, sa, x1 ? 1 : 0, gna, xp, gh, R.st);
     R.end();
     HIPCHK(hipGetLastError());
     return rrows;

@@ -36,18 +36,19 @@ namespace dmx {
 // sample, gamma, beta) — the ResBlock's mid norm_kernel launch and its hi / lo planes disappear.
 // Statistics are reduced exactly as norm_kernel reduces them and the affine + GELU is the same
 // expression, so the staged operand is bit-identical to the planes norm_kernel would have written.
-template <int BN, int EPI, int SA, int X1, int W, int GNA = 0>
-__global__ __launch_bounds__(512) void igemm_halo_kernel(const X3Params P) {
+template <int BN, int EPI, int SA, int X1, int W, int GNA = 0, int NWN = 2, int NWM = 4>
+__global__ __launch_bounds__(64 * NWM * NWN) void igemm_halo_kernel(const X3Params P) {
+  constexpr int NTH = 64 * NWM * NWN;              // threads: NWM (rows) x NWN (columns) waves
   const IgemmParams& p = P.g;
   constexpr int TR = 256 / W;                     // output image rows per tile
   constexpr int HWD = W + 2, HP = (TR + 2) * HWD;  // halo row width / pixels
   constexpr int CK = 32, RS = CK + 8;              // channels per chunk, f16 per LDS row
-  constexpr int WN = BN / 2, TM = 2, TN = WN / 32;
+  constexpr int WM = 256 / NWM, WN = BN / NWN, TM = WM / 32, TN = WN / 32;
   constexpr int PW = SA ? 8 : 4;                   // channels per staged A piece (16 bytes)
   constexpr int PPR = CK / PW;                     // pieces per halo pixel per plane
-  constexpr int NPI = (HP * PPR + 511) / 512;      // halo pieces per thread
+  constexpr int NPI = (HP * PPR + NTH - 1) / NTH;  // halo pieces per thread
   constexpr int BCH = BN * (CK / 8);               // B chunks (16 bytes) per plane per step
-  static_assert(TN >= 1 && BCH <= 512, "tile");
+  static_assert(TM >= 1 && TN >= 1 && BCH <= NTH, "tile");
 
   constexpr int LA = X1 ? 1 : HP, LB = X1 ? 1 : BN;
   __shared__ __attribute__((aligned(16))) _Float16 Ah[2][HP][RS];
@@ -56,7 +57,7 @@ __global__ __launch_bounds__(512) void igemm_halo_kernel(const X3Params P) {
   __shared__ __attribute__((aligned(16))) _Float16 Bls[2][LB][RS];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / NWN, wn = wid % NWN;
   int mt, nt, bz;
   xcd_tile(mt, nt, bz);
   const int m0 = mt * 256, n0 = nt * BN;
@@ -70,7 +71,7 @@ __global__ __launch_bounds__(512) void igemm_halo_kernel(const X3Params P) {
   short hpix[NPI], hq[NPI];
 #pragma unroll
   for (int i = 0; i < NPI; ++i) {
-    const int e = tid + 512 * i;
+    const int e = tid + NTH * i;
     const int h = e / PPR, q = e - h * PPR;
     hpix[i] = (short)h;
     hq[i] = (short)q;
@@ -145,7 +146,7 @@ __global__ __launch_bounds__(512) void igemm_halo_kernel(const X3Params P) {
 #pragma unroll
     for (int i = 0; i < NPI; ++i) {
       if (i < i0 || i >= i1) continue;
-      if (tid + 512 * i >= HP * PPR) continue;  // only the last piece index can be partial
+      if (tid + NTH * i >= HP * PPR) continue;  // only the last piece index can be partial
       const int h = hpix[i], q = hq[i];
       if constexpr (SA) {
         *reinterpret_cast<half8*>(&Ah[buf][h][q * 8]) = hah[i];
@@ -197,7 +198,7 @@ __global__ __launch_bounds__(512) void igemm_halo_kernel(const X3Params P) {
   int abase[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int r = wm * 64 + i * 32 + fr;
+    const int r = wm * WM + i * 32 + fr;
     const int ly = r / W, lx = r - ly * W;
     abase[i] = (ly + 1) * HWD + lx + 1;
   }
@@ -285,7 +286,8 @@ __global__ __launch_bounds__(512) void igemm_halo_kernel(const X3Params P) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] *= P.inv_scale;
 
   // rows of wave (wm, wn): m0 + wm * 64 + ...; the shared epilogue's 2 x 2 wave grid over 128 rows
-  igemm_epilogue<128, BN, EPI>(p, acc, 0, m0 + (wm >> 1) * 128, n0, wm & 1, wn, fr, fh);
+  igemm_epilogue<2 * WM, 2 * WN, EPI>(p, acc, 0, m0 + (wm >> 1) * 2 * WM, n0 + (wn >> 1) * 2 * WN, wm & 1, wn & 1, fr,
+                                      fh);
 }
 
 

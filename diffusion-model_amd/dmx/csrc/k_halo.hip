@@ -5,16 +5,31 @@
 
 namespace dmx {
 
-template <int BN, int SA, int X1, int W>
-static void go(int mode, int gna, const X3Params& p, dim3 grid, hipStream_t st) {
+template <int BN, int SA, int X1, int W, int NWN, int NWM>
+static void go16(int gna, const X3Params& p, dim3 grid, hipStream_t st) {
   if constexpr (SA == 0) {
     if (gna) {
-      igemm_halo_kernel<BN, EPI_STATS, 0, X1, W, 1><<<grid, 512, 0, st>>>(p);
+      igemm_halo_kernel<BN, EPI_STATS, 0, X1, W, 1, NWN, NWM><<<grid, 64 * NWN * NWM, 0, st>>>(p);
       return;
     }
   }
-  if (mode == 2) igemm_halo_kernel<BN, EPI_STATS, SA, X1, W><<<grid, 512, 0, st>>>(p);
-  else igemm_halo_bd_kernel<BN, EPI_STATS, SA, X1, W><<<grid, 512, 0, st>>>(p);
+  igemm_halo_kernel<BN, EPI_STATS, SA, X1, W, 0, NWN, NWM><<<grid, 64 * NWN * NWM, 0, st>>>(p);
+}
+
+template <int BN, int SA, int X1, int W>
+static void go(int mode, int gna, const X3Params& p, dim3 grid, hipStream_t st) {
+  // mode 4: 16-wave blocks — 4 x 4 waves of 64 x 32 (BN = 128) / 8 x 2 waves of 32 x 32 (BN = 64)
+  if (mode == 4 || mode == 5) {  // mode 5: BN = 128 as 8 x 2 waves of 32 x 64
+    if constexpr (BN == 128) {
+      if (mode == 5) go16<BN, SA, X1, W, 2, 8>(gna, p, grid, st);
+      else go16<BN, SA, X1, W, 4, 4>(gna, p, grid, st);
+    } else {
+      go16<BN, SA, X1, W, 2, 8>(gna, p, grid, st);
+    }
+    return;
+  }
+  if (mode == 1 && !gna) igemm_halo_bd_kernel<BN, EPI_STATS, SA, X1, W><<<grid, 512, 0, st>>>(p);
+  else go16<BN, SA, X1, W, 2, 4>(gna, p, grid, st);
 }
 
 template <int SA, int X1>
