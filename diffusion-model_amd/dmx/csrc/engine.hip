@@ -415,8 +415,10 @@ struct Packer {
     m->owned.push_back(l);
     c.Bh = static_cast<_Float16*>(h);
     c.Bl = static_cast<_Float16*>(l);
-    if (c.taps == 9 && c.phases == 1 && c.cout % 64 == 0 && c.cin % 32 == 0 && c.kpad == 9 * c.cin) {
-      // halo-kernel candidate (gemm(): 3x3, Cout % 64, whole 32-channel chunks)
+    if ((c.taps == 9 && c.phases == 1 && c.cout % 64 == 0 && c.cin % 32 == 0 && c.kpad == 9 * c.cin) ||
+        (c.taps == 1 && c.phases == 1)) {
+      // halo-kernel candidate (gemm(): 3x3, Cout % 64, whole 32-channel chunks) or a Linear read
+      // by the token kernels (tokmlp.h tok_gemm: one coalesced 1 KB load per B fragment)
       HIPCHK(hipMalloc(&h, n * sizeof(_Float16)));
       m->owned.push_back(h);
       HIPCHK(hipMalloc(&l, n * sizeof(_Float16)));
@@ -1188,7 +1190,19 @@ static void attention_core(Run& R, const float* qkv, float* out, int N, int L, i
   HIPCHK(hipGetLastError());
 }
 
-static TokW tokw(const ConvW& c) { return TokW{c.Bh, c.Bl, c.bias, c.inv_scale, c.kpad}; }
+// DMX_TOK_FRAG=0: token kernels read B fragments from the [Npad][Kpad] planes (32 rows per load)
+// instead of the fragment-ordered copies (same-box A/B).
+static bool tok_frag_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("DMX_TOK_FRAG");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return v;
+}
+static TokW tokw(const ConvW& c) {
+  return TokW{c.Bh, c.Bl, c.bias, c.inv_scale, c.kpad, tok_frag_enabled() ? c.Fh : nullptr,
+              tok_frag_enabled() ? c.Fl : nullptr};
+}
 
 // Fused token kernels (tokmlp.h) for the split-precision modes: TA -> attention core -> TB.
 static float* attn_block_fused(Run& R, const AttnW& a, const float* x, int N, int H, int W) {

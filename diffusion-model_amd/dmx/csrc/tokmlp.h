@@ -33,6 +33,8 @@ struct TokW {                 // one Linear in the x3 B layout
   const float* bias;          // [N]
   float inv_scale;
   int kpad;
+  const _Float16* fh;         // the same planes in MFMA-fragment order (igemm_halo.h
+  const _Float16* fl;         // frag_planes_kernel), or null
 };
 
 struct TokParams {
@@ -159,15 +161,22 @@ DMX_DEV void tok_gemm(const _Float16 (*Ah)[C + 8], const _Float16 (*Al)[C + 8], 
   for (int j = 0; j < NT; ++j)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-  const _Float16* wh = w.h + (size_t)(nw + fr) * w.kpad + 8 * fh;
-  const _Float16* wl = w.l + (size_t)(nw + fr) * w.kpad + 8 * fh;
-  const size_t jstride = (size_t)32 * w.kpad;
+  // fragment-ordered planes: fragment (column block nb, k16 step s) is 1 KB contiguous, lane-major
+  // (one coalesced load per wave); otherwise 32 rows x 32 bytes of the [Npad][Kpad] planes
+  const bool frag = w.fh != nullptr;
+  const int lane = 32 * fh + fr;
+  const _Float16* wh = frag ? w.fh + (size_t)(nw >> 5) * (w.kpad / 16) * 512 + lane * 8
+                            : w.h + (size_t)(nw + fr) * w.kpad + 8 * fh;
+  const _Float16* wl = frag ? w.fl + (size_t)(nw >> 5) * (w.kpad / 16) * 512 + lane * 8
+                            : w.l + (size_t)(nw + fr) * w.kpad + 8 * fh;
+  const size_t jstride = frag ? (size_t)(w.kpad / 16) * 512 : (size_t)32 * w.kpad;
+  const int sstride = frag ? 512 : 16;
   half8 bh[PD][NT], bl[PD][NT];
   auto loadb = [&](int s, half8* h, half8* l) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      h[j] = *reinterpret_cast<const half8*>(wh + j * jstride + 16 * s);
-      if constexpr (!X1) l[j] = *reinterpret_cast<const half8*>(wl + j * jstride + 16 * s);
+      h[j] = *reinterpret_cast<const half8*>(wh + j * jstride + sstride * s);
+      if constexpr (!X1) l[j] = *reinterpret_cast<const half8*>(wl + j * jstride + sstride * s);
     }
   };
 #pragma unroll
