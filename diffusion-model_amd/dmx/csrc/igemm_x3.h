@@ -68,16 +68,19 @@ DMX_DEV void split2(f32x2 v, unsigned& h, unsigned& l) { split2u(v.x, v.y, h, l)
 
 // X1 = 1: config-4 fp16 arithmetic — operands rounded to f16 (hi planes only), ONE MFMA per
 // product (ah*bh), fp32 accumulate; the lo planes are neither loaded nor stored.
-template <int BM, int BN, int EPI, int BK = 32, int NBUF = 2, int SPLIT_A = 0, int X1 = 0>
-__global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
+// NW = 4: 2 x 2 waves of (BM/2) x (BN/2); NW = 8: 2 x 4 waves of (BM/2) x (BN/4) (twice the waves
+// in flight per block for the latency-bound split-K launches at 8x8 / 4x4).
+template <int BM, int BN, int EPI, int BK = 32, int NBUF = 2, int SPLIT_A = 0, int X1 = 0, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void igemm_x3_kernel(const X3Params P) {
   const IgemmParams& p = P.g;
-  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
+  constexpr int NTH = 64 * NW, NWN = NW / 2;
+  constexpr int WM = BM / 2, WN = BN / NWN, TM = WM / 32, TN = WN / 32;
   constexpr int RS = BK + 8;                 // f16 per LDS row (16-byte pad)
   constexpr int APR = SPLIT_A ? BK / 8 : BK / 4;  // A pieces per row (8 f16 per plane | 4 fp32)
   constexpr int BPR = BK / 8;                // 16-byte chunks per B row per plane
-  constexpr int AP = BM * APR / 256;
-  constexpr int BP = BN * BPR / 256;
-  constexpr int ARS = 256 / APR, BRS = 256 / BPR;  // rows covered per pass
+  constexpr int AP = BM * APR / NTH;
+  constexpr int BP = BN * BPR / NTH;
+  constexpr int ARS = NTH / APR, BRS = NTH / BPR;  // rows covered per pass
   static_assert(TM >= 1 && TN >= 1 && AP >= 1 && BP >= 1, "tile");
 
   constexpr int LA = X1 ? 1 : BM, LB = X1 ? 1 : BN;  // lo planes (unused with X1)
@@ -87,7 +90,7 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
   __shared__ __attribute__((aligned(16))) _Float16 Bls[NBUF][LB][RS];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid / NWN, wn = wid % NWN;
   int mt, nt, bz;
   xcd_tile(mt, nt, bz);
   const int phase = EPI == EPI_PARTIAL ? 0 : bz;
@@ -303,7 +306,8 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(const X3Params P) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] *= P.inv_scale;
 
-  igemm_epilogue<BM, BN, EPI>(p, acc, phase, m0, n0, wm, wn, fr, fh);
+  // the shared epilogue's 2 x 2 wave grid: column pairs of waves as separate BN / (NW / 2) halves
+  igemm_epilogue<BM, 2 * WN, EPI>(p, acc, phase, m0, n0 + (wn >> 1) * 2 * WN, wm, wn & 1, fr, fh);
 }
 
 static __global__ void split_weights_kernel(const float* src, _Float16* hi, _Float16* lo, size_t n, float scale) {

@@ -2,6 +2,8 @@
 // own translation unit (k_*.hip) so the library builds in parallel; engine.hip only calls
 // these functions.
 #pragma once
+#include <cstdlib>
+
 #include "common.h"
 #include "igemm.h"
 #include "igemm_x3.h"
@@ -13,6 +15,16 @@ namespace dmx {
 // x1 = config-4 fp16 arithmetic.  k_x3_stats.hip (EPI_STATS), k_x3_part.hip (EPI_PARTIAL),
 // k_x3_epi.hip (EPI_BIAS / EPI_BIAS_GELU / EPI_BIAS_RES).
 void launch_x3_stats(int bm, int bn, int sa, int x1, const X3Params& p, dim3 grid, hipStream_t st);
+// waves per block of the EPI_STATS / EPI_PARTIAL instances: 0 (default) 8 for 128 x 128 tiles
+// (up1.0: -3 %, same-box A/B) and 4 otherwise (the 64 x 128 split-K tiles at 4x4 / 8x8 are at
+// parity or slower with 8); 4 or 8 force one (DMX_X3_WAVES).
+inline int x3_waves() {
+  static const int v = [] {
+    const char* e = std::getenv("DMX_X3_WAVES");
+    return e == nullptr ? 0 : std::atoi(e);
+  }();
+  return v;
+}
 void launch_x3_partial(int bm, int bn, int sa, int x1, const X3Params& p, dim3 grid, hipStream_t st);
 void launch_x3_epi(int epi, int bm, int bn, int sa, int x1, const X3Params& p, dim3 grid, hipStream_t st);
 // 512-thread ping-pong split-precision GEMM (igemm_pp.h), EPI_STATS, 256 x bn tiles.
