@@ -8,18 +8,23 @@
 set -e
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-TAG=${TAG:-r02}
+TAG=${TAG:-r03}
 OUT=gpurun_out/profiles
 mkdir -p $OUT
 ARGS="--steps 10 --warmup 2 --cpu-steps 0 --config4-steps 0 --config5-steps 0 --legs-steps 0 --png-steps 0 --train-steps 0 --no-e2e --sharded-T 0"
 PMC_ARGS="$ARGS --no-profile"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/prof_trace.log 2>&1
 cp "$(find gpurun_out/prof_trace -name '*kernel_stats.csv' | head -1)" $OUT/${TAG}_kernel_stats.csv
+# one graph-replayed step, dispatch by dispatch (device timestamps)
+python3 tools/trace_step.py gpurun_out/prof_trace $OUT/${TAG}_trace_step.json > $OUT/${TAG}_trace_step.txt
 rm -f gpurun_out/prof_trace/*kernel_trace.csv
+# eager HIP-event breakdown of one step (bench.py DMX_BENCH_BREAKDOWN) and the bench line of this build
+DMX_BENCH_BREAKDOWN=$OUT/${TAG}_breakdown.json timeout -k 10 300 python3 bench.py --cpu-steps 0 --train-steps 0 --png-steps 0 > $OUT/${TAG}_bench_noprof.jsonl 2> gpurun_out/bench_noprof.err
 echo "[profile] trace ok"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch -o run --output-format csv -- python3 bench.py $PMC_ARGS > gpurun_out/prof_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write -o run --output-format csv -- python3 bench.py $PMC_ARGS > gpurun_out/prof_write.log 2>&1
 python3 tools/pmc_traffic.py gpurun_out/prof_fetch gpurun_out/prof_write $OUT/${TAG}_pmc_traffic.json > gpurun_out/pmc_traffic.txt
+cp $OUT/${TAG}_pmc_traffic.json $OUT/pmc_traffic.json  # bench.py reads this one (lib_sha256-stamped)
 echo "[profile] traffic ok"
 i=0
 for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES" \
