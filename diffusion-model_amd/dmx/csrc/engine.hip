@@ -734,6 +734,14 @@ static int halo_mode() {
   return v;
 }
 static bool halo_enabled() { return halo_mode() != 0; }
+// Grids with fewer blocks than this split K (DMX_SPLIT_BELOW, same-box A/B; default 512 = 2 / CU).
+static int split_below() {
+  static const int v = [] {
+    const char* e = std::getenv("DMX_SPLIT_BELOW");
+    return e == nullptr ? 512 : std::atoi(e);
+  }();
+  return v;
+}
 static bool gn_fuse_enabled() {
   static const bool v = [] {
     const char* e = std::getenv("DMX_GN_FUSE");
@@ -794,6 +802,7 @@ struct GnLoad {
   int cnt = 0;
   const float* gamma = nullptr;
   const float* beta = nullptr;
+  const float* res = nullptr;       // non-null: GELU(res + GroupNorm(x)) (residual ResBlock output)
 };
 
 // Output-channel tile of the halo-staged 3x3 conv for this GEMM, or 0 when it does not apply
@@ -833,7 +842,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   const int bk = pp ? 32 : x3 ? 64 : IG_BK;
   const int nkt = cw.kpad / bk;
   int splits = 1, ksplit = nkt;
-  if (!hbn && !pp && cw.phases == 1 && blocks < 512 && nkt * bk >= 512) {  // split K below 2 blocks / CU
+  if (!hbn && !pp && cw.phases == 1 && blocks < split_below() && nkt * bk >= 512) {  // split K below 2 blocks / CU
     splits = std::min(std::min(8, std::max(2, 512 / blocks)), nkt * bk / 256);
     ksplit = cdiv(nkt, splits);
     splits = cdiv(nkt, ksplit);
@@ -903,6 +912,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   xp.gn_rowpart = nullptr;
   xp.gn_cnt = 0;
   xp.gn_gamma = xp.gn_beta = nullptr;
+  xp.gn_res = nullptr;
   {
     const size_t a_el = (size_t)N * p.Hin * p.Win * s.C;
     const size_t ab = a_el * (ash != nullptr ? 2 : 4), bb = (size_t)cw.npad * cw.kpad * 2;
@@ -944,12 +954,13 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   }
   if (hbn) {  // halo-staged 3x3 conv, 256-pixel x hbn tiles (igemm_halo.h)
     dim3 gh(M / 256, cw.cout / hbn, 1);
-    const int gna = gn != nullptr ? 1 : 0;
+    const int gna = gn != nullptr ? (gn->res != nullptr ? 2 : 1) : 0;
     if (gna) {
       xp.gn_rowpart = gn->rowpart;
       xp.gn_cnt = gn->cnt;
       xp.gn_gamma = gn->gamma;
       xp.gn_beta = gn->beta;
+      xp.gn_res = gn->res;
     }
     std::snprintf(nm, sizeof nm, "igemm_halo_kernel<%d, %d, %d, %d, %d, %d>", hbn, (int)EPI_STATS, sa, x1 ? 1 : 0, W,
                   gna);
@@ -1074,10 +1085,15 @@ static NormParams norm_params(const float* raw, const float2* rowpart, int nseg,
 // in_h / in_l: `in` is available as f16 hi / lo planes (conv1 then reads those).
 // planes_out: the output only feeds the next ResBlock's conv1 — write it as hi / lo planes
 // (same bytes as fp32) when the split GEMM can use them; *wrote_planes reports the choice.
+// defer_out (residual blocks whose conv2 wrote whole-sample partials): the final GroupNorm +
+// residual + GELU is NOT launched; the raw conv2 output is returned and *defer_out describes the
+// normalisation for the consumer (the next ResBlock's halo conv1, GNA = 2); defer_out->rowpart
+// stays null when the block could not defer.  gn_in: `in` is such a deferred raw output (conv1
+// applies it while staging; the block must not be residual).
 static float* resblock(Run& R, const ResW& w, const SrcDesc& in, int mode, int N, int H, int W, bool residual,
                        const float* emb, int emb_stride, int emb_off, int n_out = 0,
                        const _Float16* in_h = nullptr, const _Float16* in_l = nullptr, bool planes_out = false,
-                       bool* wrote_planes = nullptr) {
+                       bool* wrote_planes = nullptr, GnLoad* defer_out = nullptr, const GnLoad* gn_in = nullptr) {
   const int M = N * H * W, HW = H * W;
   if (n_out <= 0) n_out = N;
   const int seg = 32;
@@ -1089,7 +1105,9 @@ static float* resblock(Run& R, const ResW& w, const SrcDesc& in, int mode, int N
   float2* rp2 = R.ws.get<float2>((size_t)M * (w.cout / seg));
   float* out = R.ws.get<float>((size_t)n_out * HW * w.cout);
   Deferred d1, d2;  // split-K convs at low resolution: reduce + GroupNorm in one launch
-  const int rr1 = gemm(R, in, mode, N, H, W, w.c1, EPI_STATS, r1, nullptr, rp1, seg, in_h, in_l, &d1);
+  if (gn_in != nullptr && (residual || mode != SRC_PLAIN))
+    throw Error(DMX_E_INTERNAL, "resblock: a GroupNorm-on-load input needs a plain, non-residual block");
+  const int rr1 = gemm(R, in, mode, N, H, W, w.c1, EPI_STATS, r1, nullptr, rp1, seg, in_h, in_l, &d1, gn_in);
   NormParams n1 = norm_params(r1, rp1, w.mid / seg, rr1, w.g1.p, w.b1.p, w.mid, HW, a1);
   n1.act = 1;
   _Float16* a1h = reinterpret_cast<_Float16*>(a1);
@@ -1118,6 +1136,17 @@ static float* resblock(Run& R, const ResW& w, const SrcDesc& in, int mode, int N
     else norm(R, n1, N);
     rr2 = gemm(R, plain_src(a1, w.mid), SRC_PLAIN, N, H, W, w.c2, EPI_STATS, r2, nullptr, rp2, seg,
                planes ? a1h : nullptr, planes ? a1l : nullptr, &d2);
+  }
+  if (defer_out != nullptr) *defer_out = GnLoad{};
+  if (defer_out != nullptr && residual && mode == SRC_PLAIN && !d2.fused && emb == nullptr && n_out == N &&
+      !R.m->debug) {
+    defer_out->rowpart = rp2;
+    defer_out->cnt = rr2 * (w.cout / seg);
+    defer_out->gamma = w.g2.p;
+    defer_out->beta = w.b2.p;
+    defer_out->res = in.src0;
+    if (wrote_planes != nullptr) *wrote_planes = false;
+    return r2;
   }
   NormParams n2 = norm_params(r2, rp2, w.cout / seg, rr2, w.g2.p, w.b2.p, w.cout, HW, out);
   if (residual) {
@@ -1427,12 +1456,20 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
     _Float16* cat_l = cat_planes ? cat_h + cat_el : nullptr;
     prep<SRC_UPCAT>(R, u, cat, N, sh[si], sw[si], "prep_kernel<3>", cat_h, cat_l);
     bool hp = false;
+    // r0's final GroupNorm + residual + GELU folded into r1's halo conv1 where that conv runs the
+    // halo kernel (igemm_halo.h GNA = 2): one norm_kernel launch and the h0 round trip fewer
+    GnLoad dly;
+    const bool try_defer = gn_fuse_enabled() && !R.m->debug && R.m->prec >= 1 &&
+                           halo_bn(R, u.C, N, sh[si], sw[si], m->up[i].r1.c1, EPI_STATS, true) > 0;
     float* h0 = resblock(R, m->up[i].r0, plain_src(cat, u.C), SRC_PLAIN, N, sh[si], sw[si], true, nullptr, 0, 0, 0,
-                         cat_h, cat_l, m->up[i].r1.c1.Bh != nullptr, &hp);
+                         cat_h, cat_l, m->up[i].r1.c1.Bh != nullptr, &hp, try_defer ? &dly : nullptr);
     R.layer = "up" + std::to_string(i + 1) + ".1";
     const _Float16* h0h = hp ? reinterpret_cast<const _Float16*>(h0) : nullptr;
-    float* h1 = resblock(R, m->up[i].r1, plain_src(h0, u.C), SRC_PLAIN, N, sh[si], sw[si], false, emb, m->hsum,
-                         m->up[i].emb_off, 0, h0h, hp ? h0h + (size_t)N * sh[si] * sw[si] * u.C : nullptr);
+    float* h1 = dly.rowpart != nullptr
+                    ? resblock(R, m->up[i].r1, plain_src(h0, u.C), SRC_PLAIN, N, sh[si], sw[si], false, emb, m->hsum,
+                               m->up[i].emb_off, 0, nullptr, nullptr, false, nullptr, nullptr, &dly)
+                    : resblock(R, m->up[i].r1, plain_src(h0, u.C), SRC_PLAIN, N, sh[si], sw[si], false, emb, m->hsum,
+                               m->up[i].emb_off, 0, h0h, hp ? h0h + (size_t)N * sh[si] * sw[si] * u.C : nullptr);
     ch = sh[si];
     cw = sw[si];
     cc = m->up[i].cout;

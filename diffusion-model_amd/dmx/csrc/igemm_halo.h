@@ -34,8 +34,10 @@ namespace dmx {
 // GNA = 1: the source is a raw conv output (fp32, SA = 0) whose GroupNorm(1, C) + GELU is applied
 // while the halo is staged (P.gn_*: the producing conv's (sum, sum of squares) partials of each
 // sample, gamma, beta) — the ResBlock's mid norm_kernel launch and its hi / lo planes disappear.
-// Statistics are reduced exactly as norm_kernel reduces them and the affine + GELU is the same
-// expression, so the staged operand is bit-identical to the planes norm_kernel would have written.
+// GNA = 2: GELU(P.gn_res + GroupNorm(source)) — the output of a residual ResBlock (models/
+// unet_cond.py:25-26) consumed by the next ResBlock's conv1, its final norm_kernel folded in here.
+// Statistics are reduced exactly as norm_kernel reduces them and the affine (+ residual) + GELU is
+// the same expression, so the staged operand is bit-identical to what norm_kernel would write.
 template <int BN, int EPI, int SA, int X1, int W, int GNA = 0, int NWN = 2, int NWM = 4>
 __global__ __launch_bounds__(64 * NWM * NWN) void igemm_halo_kernel(const X3Params P) {
   constexpr int NTH = 64 * NWM * NWN;              // threads: NWM (rows) x NWN (columns) waves
@@ -125,7 +127,9 @@ __global__ __launch_bounds__(64 * NWM * NWN) void igemm_halo_kernel(const X3Para
   }
   // register stages (B: two sets, a step's slice is loaded two steps before it is read)
   floatx4 ha4[SA ? 1 : NPI];
+  floatx4 hr4[GNA == 2 ? NPI : 1];  // residual pieces (GNA = 2)
   half8 hah[SA ? NPI : 1], hal[SA ? NPI : 1];
+  const __amdgpu_buffer_rsrc_t rRes = rsrc_of(GNA == 2 ? (const void*)P.gn_res : (const void*)p.src.src0, P.a_bytes);
   half8 rbh[2], rbl[2];
   auto load_halo = [&](int c) {
 #pragma unroll
@@ -136,6 +140,7 @@ __global__ __launch_bounds__(64 * NWM * NWN) void igemm_halo_kernel(const X3Para
         if constexpr (!X1) hal[i] = bload_h8(rAl, off, 0);
       } else {
         ha4[i] = bload_f4(rAh, off, 0);
+        if constexpr (GNA == 2) hr4[i] = bload_f4(rRes, off, 0);
       }
     }
   };
@@ -153,9 +158,13 @@ __global__ __launch_bounds__(64 * NWM * NWN) void igemm_halo_kernel(const X3Para
         if constexpr (!X1) *reinterpret_cast<half8*>(&Al[buf][h][q * 8]) = hal[i];
       } else {
         floatx4 v = ha4[i];
-        if constexpr (GNA) {  // GroupNorm + GELU of the raw source; zero padding stays zero
+        if constexpr (GNA) {  // GroupNorm (+ residual) + GELU of the raw source; zero padding stays zero
           const int ch = cst + q * 4;
-          v = gn_apply4v(v, gst, ld4(P.gn_gamma + ch), ld4(P.gn_beta + ch), 1);
+          v = gn_apply4v(v, gst, ld4(P.gn_gamma + ch), ld4(P.gn_beta + ch), GNA == 1 ? 1 : 0);
+          if constexpr (GNA == 2) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = gelu(hr4[i][j] + v[j]);
+          }
           if (hoff[i] < 0) v = floatx4{0.f, 0.f, 0.f, 0.f};
         }
         if constexpr (X1) {

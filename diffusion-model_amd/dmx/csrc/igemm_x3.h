@@ -45,6 +45,7 @@ struct X3Params {
   int gn_cnt;
   const float* gn_gamma;
   const float* gn_beta;
+  const float* gn_res;       // GNA = 2: GELU(res + GroupNorm(src)) (a residual ResBlock's output)
 };
 
 
@@ -70,7 +71,9 @@ DMX_DEV void split2(f32x2 v, unsigned& h, unsigned& l) { split2u(v.x, v.y, h, l)
 // product (ah*bh), fp32 accumulate; the lo planes are neither loaded nor stored.
 // NW = 4: 2 x 2 waves of (BM/2) x (BN/2); NW = 8: 2 x 4 waves of (BM/2) x (BN/4) (twice the waves
 // in flight per block for the latency-bound split-K launches at 8x8 / 4x4).
-template <int BM, int BN, int EPI, int BK = 32, int NBUF = 2, int SPLIT_A = 0, int X1 = 0, int NW = 4>
+// PF = 2 (NBUF = 1 only): two register stages, K-tile k + 2 is loaded while tile k computes (two
+// MFMA phases of latency cover instead of one, for the memory-latency-bound split-K launches).
+template <int BM, int BN, int EPI, int BK = 32, int NBUF = 2, int SPLIT_A = 0, int X1 = 0, int NW = 4, int PF = 1>
 __global__ __launch_bounds__(64 * NW) void igemm_x3_kernel(const X3Params P) {
   const IgemmParams& p = P.g;
   constexpr int NTH = 64 * NW, NWN = NW / 2;
@@ -115,9 +118,10 @@ __global__ __launch_bounds__(64 * NW) void igemm_x3_kernel(const X3Params P) {
     tmask[i] = tap_mask(p.geom, phase, p.taps, m, p.M, p.H, p.W, p.Hin, p.Win);
   }
 
-  floatx4 ra4[SPLIT_A ? 1 : AP];
-  half8 rah[SPLIT_A ? AP : 1], ral[SPLIT_A ? AP : 1];
-  half8 rbh[BP], rbl[BP];
+  static_assert(PF == 1 || NBUF == 1, "two register stages only with one LDS buffer");
+  floatx4 ra4[PF][SPLIT_A ? 1 : AP];
+  half8 rah[PF][SPLIT_A ? AP : 1], ral[PF][SPLIT_A ? AP : 1];
+  half8 rbh[PF][BP], rbl[PF][BP];
   // (tap, channel) of this thread's A piece, advanced incrementally (C >= BK on this path)
   int ltap = 0, lc = 0;
   auto seek = [&](int kt) {
@@ -138,7 +142,7 @@ __global__ __launch_bounds__(64 * NW) void igemm_x3_kernel(const X3Params P) {
 #pragma unroll
   for (int i = 0; i < BP; ++i) boffs[i] = ((n0 + rb + i * BRS) * p.Kpad + qb * 8) * 2;
 #endif
-  auto load_tile = [&](int kt) {
+  auto load_tile = [&](int kt, int st) {  // st: register stage (compile-time constant at every call)
     int ddy, ddx;
     tap_offset(p.geom, phase, ltap, ddy, ddx);
     const int delta = ddy * p.Win + ddx;
@@ -158,55 +162,55 @@ __global__ __launch_bounds__(64 * NW) void igemm_x3_kernel(const X3Params P) {
 #ifndef DMX_NO_BUFLOAD
       const int boff_a = ok ? off * AES : kOOB;
       if constexpr (SPLIT_A) {
-        rah[i] = bload_h8(rAh, boff_a, 0);
-        if constexpr (!X1) ral[i] = bload_h8(rAl, boff_a, 0);
+        rah[st][i] = bload_h8(rAh, boff_a, 0);
+        if constexpr (!X1) ral[st][i] = bload_h8(rAl, boff_a, 0);
       } else {
-        ra4[i] = bload_f4(rAh, boff_a, 0);
+        ra4[st][i] = bload_f4(rAh, boff_a, 0);
       }
 #else
       if constexpr (SPLIT_A) {
         const _Float16* ph = ok ? P.Ash + off : reinterpret_cast<const _Float16*>(g_zero16);
-        rah[i] = *reinterpret_cast<const half8*>(ph);
+        rah[st][i] = *reinterpret_cast<const half8*>(ph);
         if constexpr (!X1) {
           const _Float16* pl = ok ? P.Asl + off : reinterpret_cast<const _Float16*>(g_zero16);
-          ral[i] = *reinterpret_cast<const half8*>(pl);
+          ral[st][i] = *reinterpret_cast<const half8*>(pl);
         }
       } else {
-        ra4[i] = ld4(ok ? asrc + off : g_zero16);
+        ra4[st][i] = ld4(ok ? asrc + off : g_zero16);
       }
 #endif
     }
 #pragma unroll
     for (int i = 0; i < BP; ++i) {
 #ifndef DMX_NO_BUFLOAD
-      rbh[i] = bload_h8(rBh, boffs[i], kt * BK * 2);
-      if constexpr (!X1) rbl[i] = bload_h8(rBl, boffs[i], kt * BK * 2);
+      rbh[st][i] = bload_h8(rBh, boffs[i], kt * BK * 2);
+      if constexpr (!X1) rbl[st][i] = bload_h8(rBl, boffs[i], kt * BK * 2);
 #else
       const size_t o = (size_t)(n0 + rb + i * BRS) * p.Kpad + kt * BK + qb * 8;
-      rbh[i] = *reinterpret_cast<const half8*>(Bh + o);
-      if constexpr (!X1) rbl[i] = *reinterpret_cast<const half8*>(Bl + o);
+      rbh[st][i] = *reinterpret_cast<const half8*>(Bh + o);
+      if constexpr (!X1) rbl[st][i] = *reinterpret_cast<const half8*>(Bl + o);
 #endif
     }
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf, int st) {
 #pragma unroll
     for (int i = 0; i < AP; ++i) {
       if constexpr (SPLIT_A) {
-        *reinterpret_cast<half8*>(&Ah[buf][ra + i * ARS][qa * 8]) = rah[i];
-        if constexpr (!X1) *reinterpret_cast<half8*>(&Al[buf][ra + i * ARS][qa * 8]) = ral[i];
+        *reinterpret_cast<half8*>(&Ah[buf][ra + i * ARS][qa * 8]) = rah[st][i];
+        if constexpr (!X1) *reinterpret_cast<half8*>(&Al[buf][ra + i * ARS][qa * 8]) = ral[st][i];
       } else if constexpr (X1) {
-        *reinterpret_cast<half4*>(&Ah[buf][ra + i * ARS][qa * 4]) = __builtin_convertvector(ra4[i], half4);
+        *reinterpret_cast<half4*>(&Ah[buf][ra + i * ARS][qa * 4]) = __builtin_convertvector(ra4[st][i], half4);
       } else {
         half4 h, l;
-        split4(ra4[i], h, l);
+        split4(ra4[st][i], h, l);
         *reinterpret_cast<half4*>(&Ah[buf][ra + i * ARS][qa * 4]) = h;
         *reinterpret_cast<half4*>(&Al[buf][ra + i * ARS][qa * 4]) = l;
       }
     }
 #pragma unroll
     for (int i = 0; i < BP; ++i) {
-      *reinterpret_cast<half8*>(&Bhs[buf][rb + i * BRS][qb * 8]) = rbh[i];
-      if constexpr (!X1) *reinterpret_cast<half8*>(&Bls[buf][rb + i * BRS][qb * 8]) = rbl[i];
+      *reinterpret_cast<half8*>(&Bhs[buf][rb + i * BRS][qb * 8]) = rbh[st][i];
+      if constexpr (!X1) *reinterpret_cast<half8*>(&Bls[buf][rb + i * BRS][qb * 8]) = rbl[st][i];
     }
   };
 
@@ -274,25 +278,39 @@ __global__ __launch_bounds__(64 * NW) void igemm_x3_kernel(const X3Params P) {
   }
   seek(kbeg);
   if constexpr (NBUF == 2) {
-    load_tile(kbeg);
-    store_tile(0);
+    load_tile(kbeg, 0);
+    store_tile(0, 0);
     __syncthreads();
     for (int kt = 0; kt < nK; ++kt) {
       const int buf = kt & 1;
-      if (kt + 1 < nK) load_tile(kbeg + kt + 1);
+      if (kt + 1 < nK) load_tile(kbeg + kt + 1, 0);
       compute(buf);
-      if (kt + 1 < nK) store_tile(buf ^ 1);
+      if (kt + 1 < nK) store_tile(buf ^ 1, 0);
       __syncthreads();
     }
+  } else if constexpr (PF == 2) {
+    load_tile(kbeg, 0);
+    if (nK > 1) load_tile(kbeg + 1, 1);
+    auto body = [&](int kt, int st) {
+      store_tile(0, st);
+      __syncthreads();
+      if (kt + 2 < nK) load_tile(kbeg + kt + 2, st);  // the stage just written is free again
+      compute(0);
+      __syncthreads();
+    };
+    for (int kt = 0; kt < nK; kt += 2) {
+      body(kt, 0);
+      if (kt + 1 < nK) body(kt + 1, 1);
+    }
   } else {
-    load_tile(kbeg);
+    load_tile(kbeg, 0);
     for (int kt = 0; kt < nK; ++kt) {
-      store_tile(0);
+      store_tile(0, 0);
       __syncthreads();
 #if DMX_DIAG_GEMM == 2  // diagnostic build only (wrong results): no global loads after the first tile
       if (false)
 #endif
-      if (kt + 1 < nK) load_tile(kbeg + kt + 1);  // in flight during the MFMAs
+      if (kt + 1 < nK) load_tile(kbeg + kt + 1, 0);  // in flight during the MFMAs
 #if DMX_DIAG_GEMM != 1  // diagnostic build only (wrong results): no MFMAs / fragment reads
       compute(0);
 #endif
@@ -589,8 +607,18 @@ __host__ __device__ inline size_t att16_lds_bytes(int L, int x1) {
   return 2 * ((x1 ? 1 : 2) * lp * 16 + (x1 ? 18 : 35) * vs);
 }
 
+// Cross-half (lanes l and l ^ 32) max with v_permlane32_swap (a VALU op; __shfl_xor(v, 32) is a
+// ds_bpermute round trip through the LDS pipe on the softmax's critical path).
+DMX_DEV float max_halves(float v) {
+  const unsigned u = __builtin_bit_cast(unsigned, v);
+  const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
+}
+
+// stag > 0: the waves with (wid >> 2) odd (one of each SIMD's wave pairs) start stag x 64 cycles
+// late, so co-resident waves sit in different phases of the QK^T / softmax / PV sequence.
 template <int NW, int X1 = 0>
-__global__ __launch_bounds__(NW * 64) void attention16_kernel(const float* qkv, float* out, int L, int C) {
+__global__ __launch_bounds__(NW * 64) void attention16_kernel(const float* qkv, float* out, int L, int C, int stag) {
   constexpr int D = 16;
   extern __shared__ __attribute__((aligned(16))) _Float16 att_lds[];
   const int Lp = att16_lp(L), VS = Lp + 8;
@@ -650,6 +678,8 @@ __global__ __launch_bounds__(NW * 64) void attention16_kernel(const float* qkv, 
   const _Float16* vrh = Vh + (fr < 16 ? fr : fr == 16 ? 16 : 17) * VS;  // this lane's V^T row (hi)
   const _Float16* vrl = Vl + (fr < 16 ? fr : 16) * VS;                  // (lo)
   const int nqt = (L + 31) / 32;
+  if ((wid >> 2) & 1)
+    for (int i = 0; i < stag; ++i) __builtin_amdgcn_s_sleep(1);
   for (int qt = wid; qt < nqt; qt += NW) {
     const int q = qt * 32 + fr;
     half8 qh, ql;
@@ -704,7 +734,7 @@ __global__ __launch_bounds__(NW * 64) void attention16_kernel(const float* qkv, 
       float mx = sc[0];
 #pragma unroll
       for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sc[r]);
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = max_halves(mx);
       if (c0 == 0 || mx > TAU) {  // move the reference to this chunk's max (rare after the first)
         const float alpha = __builtin_amdgcn_exp2f(-mx);
 #pragma unroll

@@ -25,7 +25,11 @@ static hipError_t go16(const float* qkv, float* out, int L, int C, int N, hipStr
     if (e != hipSuccess) return e;
     granted = bytes;
   }
-  attention16_kernel<NW, X1><<<dim3(1, 4, N), NW * 64, bytes, st>>>(qkv, out, L, C);
+  static const int stag = [] {  // DMX_ATT_STAGGER (same-box A/B): start offset of half the waves
+    const char* e = std::getenv("DMX_ATT_STAGGER");
+    return e == nullptr ? 0 : std::atoi(e);
+  }();
+  attention16_kernel<NW, X1><<<dim3(1, 4, N), NW * 64, bytes, st>>>(qkv, out, L, C, stag);
   return hipSuccess;
 }
 

@@ -8,8 +8,12 @@ namespace dmx {
 template <int BN, int SA, int X1, int W, int NWN, int NWM>
 static void go16(int gna, const X3Params& p, dim3 grid, hipStream_t st) {
   if constexpr (SA == 0) {
-    if (gna) {
+    if (gna == 1) {
       igemm_halo_kernel<BN, EPI_STATS, 0, X1, W, 1, NWN, NWM><<<grid, 64 * NWN * NWM, 0, st>>>(p);
+      return;
+    }
+    if (gna == 2) {
+      igemm_halo_kernel<BN, EPI_STATS, 0, X1, W, 2, NWN, NWM><<<grid, 64 * NWN * NWM, 0, st>>>(p);
       return;
     }
   }

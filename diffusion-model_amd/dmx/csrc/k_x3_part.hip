@@ -11,7 +11,8 @@ static void go(const X3Params& p, dim3 grid, hipStream_t st) {
       return;
     }
   }
-  igemm_x3_kernel<BM, BN, EPI_PARTIAL, 64, 1, SA, X1><<<grid, 256, 0, st>>>(p);
+  if (x3_prefetch() == 2) igemm_x3_kernel<BM, BN, EPI_PARTIAL, 64, 1, SA, X1, 4, 2><<<grid, 256, 0, st>>>(p);
+  else igemm_x3_kernel<BM, BN, EPI_PARTIAL, 64, 1, SA, X1><<<grid, 256, 0, st>>>(p);
 }
 
 template <int SA, int X1>

@@ -35,6 +35,14 @@ void launch_pp(int bn, int sa, int x1, const X3Params& p, dim3 grid, hipStream_t
 // per channel chunk); mode 2: B staged in LDS per step (one barrier per step).
 // gna = 1 (mode 2, sa = 0): GroupNorm + GELU of the raw source applied while staging.
 void launch_halo(int mode, int bn, int w, int sa, int x1, int gna, const X3Params& p, dim3 grid, hipStream_t st);
+// register-stage depth of the 4-wave EPI_STATS / EPI_PARTIAL instances (1 or 2; DMX_X3_PF)
+inline int x3_prefetch() {
+  static const int v = [] {
+    const char* e = std::getenv("DMX_X3_PF");
+    return e == nullptr ? 1 : std::atoi(e);
+  }();
+  return v;
+}
 // exact-fp32 MFMA implicit GEMM (igemm.h), k_f32.hip.
 void launch_f32(int src_mode, int epi, int bm, int bn, const IgemmParams& p, dim3 grid, hipStream_t st);
 // attention cores (k_attn.hip): split-precision (D, waves-per-EU hint, x1) and exact fp32 (D, QT).
