@@ -29,7 +29,9 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-u
 # Per-translation-unit flags.  The attention cores keep their softmax in scalar f32 VALU: the
 # SLP vectoriser would pack it into v_pk_add / v_pk_mul_f32, whose issue cost beside MFMAs is
 # far above that of the two scalar halves (MI355X_MICROARCH.md, constants table).
-FILE_FLAGS = {"k_attn.hip": ["-fno-slp-vectorize"]}
+# No NaN semantics there either: fmaxf needs no canonicalising v_max x, x, x per operand (the
+# scores are finite or the -inf of a masked key).
+FILE_FLAGS = {"k_attn.hip": ["-fno-slp-vectorize", "-fno-honor-nans"]}
 
 
 def _newest_header() -> float:

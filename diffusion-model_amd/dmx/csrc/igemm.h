@@ -126,10 +126,15 @@ constexpr int IG_LDS_STRIDE = 20;  // floats per LDS row (16 + 4 pad)
 // Shared epilogue of the implicit GEMMs: accumulators (C/D layout of the 32x32 MFMA:
 // col = lane&31, row = (r&3) + 8(r>>2) + 4(lane>>5)) -> split-K slab | output (+bias,
 // GELU, residual) and GroupNorm partials.
-template <int BM, int BN, int EPI>
+// RPERM = 1: the A operand's fragment rows 16..31 were read in the rotated order of
+// igemm_halo_kernel<W = 16> (fragment row i >= 16 holds tile row 16 + ((i - 18) & 15)).
+template <int BM, int BN, int EPI, int RPERM = 0>
 DMX_DEV void igemm_epilogue(const IgemmParams& p, floatx16 (&acc)[BM / 64][BN / 64], int phase, int m0, int n0,
                             int wm, int wn, int fr, int fh) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
+  // RPERM: tile row of fragment row i = (r & 3) + 8 (r >> 2) + 4 fh is i + adj, adj = 14 for
+  // i = 16, 17 (r = 8, 9 with fh = 0), -2 for the other i >= 16 (r >= 8), 0 below
+#define rperm_adj(r) ((RPERM && (r) >= 8) ? (((r) <= 9 && fh == 0) ? 14 : -2) : 0)
   const int HW = p.H * p.W;
   if constexpr (EPI == EPI_PARTIAL) {
     float* dst = p.partial + (size_t)blockIdx.z * p.M * p.Cout;
@@ -137,7 +142,7 @@ DMX_DEV void igemm_epilogue(const IgemmParams& p, floatx16 (&acc)[BM / 64][BN / 
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh;
+        const int m = m0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * fh + rperm_adj(r);
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int col = n0 + wn * WN + j * 32 + fr;
@@ -164,7 +169,7 @@ DMX_DEV void igemm_epilogue(const IgemmParams& p, floatx16 (&acc)[BM / 64][BN / 
       const int mb = m0 + wm * WM + i * 32;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int m = mb + (r & 3) + 8 * (r >> 2) + 4 * fh;
+        const int m = mb + (r & 3) + 8 * (r >> 2) + 4 * fh + rperm_adj(r);
         const bool mv = m < p.M;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -213,7 +218,7 @@ DMX_DEV void igemm_epilogue(const IgemmParams& p, floatx16 (&acc)[BM / 64][BN / 
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = (r & 3) + 8 * (r >> 2) + 4 * fh;
-      const int m = m0 + wm * WM + i * 32 + row;
+      const int m = m0 + wm * WM + i * 32 + row + rperm_adj(r);
       const bool mv = m < p.M;
       size_t oidx = (size_t)m;
       int nn = 0, rr = 0;
@@ -275,6 +280,7 @@ DMX_DEV void igemm_epilogue(const IgemmParams& p, floatx16 (&acc)[BM / 64][BN / 
       }
     }
   }
+#undef rperm_adj
 }
 
 template <int BM, int BN, int SRC, int EPI>

@@ -203,11 +203,18 @@ __global__ __launch_bounds__(64 * NWM * NWN) void igemm_halo_kernel(const X3Para
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int fr = lane & 31, fh = lane >> 5;
-  // halo pixel of each A fragment row for tap (0, 0): output pixel r = wm*64 + i*32 + fr of the tile
+  // halo pixel of each A fragment row for tap (0, 0): output pixel r = wm*64 + i*32 + fp of the
+  // tile.  W = 16: a fragment spans two image rows, whose halo rows lie 18 LDS rows apart; lanes
+  // 16..31 take the second row rotated by two pixels (fp = 16 + ((fr - 18) & 15)) so that every
+  // 16-lane group of ds_read_b128 (lanes {0-3,12-15,20-27}, {4-11,16-19,28-31}) reads 16 LDS rows
+  // distinct mod 16 — distinct 16-byte slots of the 80-byte-row layout, no bank conflict.  The
+  // epilogue writes accumulator rows back through the same rotation (igemm_epilogue RPERM).
+  constexpr int RPERM = W == 16 ? 1 : 0;
+  const int fp = (RPERM && fr >= 16) ? 16 + ((fr - 18) & 15) : fr;
   int abase[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int r = wm * WM + i * 32 + fr;
+    const int r = wm * WM + i * 32 + fp;
     const int ly = r / W, lx = r - ly * W;
     abase[i] = (ly + 1) * HWD + lx + 1;
   }
@@ -295,8 +302,8 @@ __global__ __launch_bounds__(64 * NWM * NWN) void igemm_halo_kernel(const X3Para
       for (int r = 0; r < 16; ++r) acc[i][j][r] *= P.inv_scale;
 
   // rows of wave (wm, wn): m0 + wm * 64 + ...; the shared epilogue's 2 x 2 wave grid over 128 rows
-  igemm_epilogue<2 * WM, 2 * WN, EPI>(p, acc, 0, m0 + (wm >> 1) * 2 * WM, n0 + (wn >> 1) * 2 * WN, wm & 1, wn & 1, fr,
-                                      fh);
+  igemm_epilogue<2 * WM, 2 * WN, EPI, RPERM>(p, acc, 0, m0 + (wm >> 1) * 2 * WM, n0 + (wn >> 1) * 2 * WN, wm & 1,
+                                             wn & 1, fr, fh);
 }
 
 

@@ -597,13 +597,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 // The per-chunk staging of the 128-query kernel (two barriers per 64 keys, K / V re-read and
 // re-split by every query block of the head, 2-byte transposed V stores) is gone.
 //
-// LDS (dynamic, Lp = L rounded up to 64): Kh, Kl [Lp][16]; Vh [18][Lp + 8] (rows 0-15 V^T,
-// 16 ones, 17 zeros); Vl [17][Lp + 8] (row 16 zeros).  Lanes 16-31 of a V^T fragment read the
+// LDS (dynamic, Lp = L rounded up to 64): Kh, Kl [Lp][16]; Vh [18][Lp + 4] (rows 0-15 V^T,
+// 16 ones, 17 zeros); Vl [17][Lp + 4] (row 16 zeros).  The V^T row pitch is 2 mod 32 dwords: the
+// 16 rows a ds_read2_b64 lane group reads (banks (a/4) mod 32) cover the 32 banks exactly once.  Lanes 16-31 of a V^T fragment read the
 // constant rows instead of holding padding in LDS.  Keys in [L, Lp) are zero and masked.
 // ---------------------------------------------------------------------------
 __host__ __device__ inline int att16_lp(int L) { return (L + 63) / 64 * 64; }
 __host__ __device__ inline size_t att16_lds_bytes(int L, int x1) {
-  const size_t lp = (size_t)att16_lp(L), vs = lp + 8;
+  const size_t lp = (size_t)att16_lp(L), vs = lp + 4;
   return 2 * ((x1 ? 1 : 2) * lp * 16 + (x1 ? 18 : 35) * vs);
 }
 
@@ -615,13 +616,22 @@ DMX_DEV float max_halves(float v) {
   return fmaxf(__builtin_bit_cast(float, (unsigned)r[0]), __builtin_bit_cast(float, (unsigned)r[1]));
 }
 
+// v_mfma_f32_32x32x16_f16 with its accumulator input (the loop-invariant -mref) in other registers
+// than its result: the builtin's tied form copies negm into the result registers every chunk
+// (eight v_mov_b64 on the VALU issue port this kernel is bound by).
+DMX_DEV floatx16 mfma_untied(half8 a, half8 b, floatx16 c) {
+  floatx16 d;
+  asm("v_mfma_f32_32x32x16_f16 %0, %1, %2, %3" : "=&v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
 // stag > 0: the waves with (wid >> 2) odd (one of each SIMD's wave pairs) start stag x 64 cycles
 // late, so co-resident waves sit in different phases of the QK^T / softmax / PV sequence.
 template <int NW, int X1 = 0>
 __global__ __launch_bounds__(NW * 64) void attention16_kernel(const float* qkv, float* out, int L, int C, int stag) {
   constexpr int D = 16;
   extern __shared__ __attribute__((aligned(16))) _Float16 att_lds[];
-  const int Lp = att16_lp(L), VS = Lp + 8;
+  const int Lp = att16_lp(L), VS = Lp + 4;
   _Float16* Kh = att_lds;
   _Float16* Kl = Kh + Lp * D;
   _Float16* Vh = Kl + (X1 ? 0 : Lp * D);
@@ -718,11 +728,11 @@ __global__ __launch_bounds__(NW * 64) void attention16_kernel(const float* qkv, 
         const half8 kh = *reinterpret_cast<const half8*>(&Kh[krow]);
         if constexpr (!X1) {
           const half8 kl = *reinterpret_cast<const half8*>(&Kl[krow]);
-          sc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kl, qh, negm, 0, 0, 0);
+          sc = mfma_untied(kl, qh, negm);
           sc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, ql, sc, 0, 0, 0);
           sc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, qh, sc, 0, 0, 0);
         } else {
-          sc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, qh, negm, 0, 0, 0);
+          sc = mfma_untied(kh, qh, negm);
         }
       }
       const int nvalid = L - c0;
