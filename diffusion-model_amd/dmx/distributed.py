@@ -214,14 +214,31 @@ class ShardedCondSampler:
         return gather_rows(x, B)
 
 
+def global_mask_mean(mask: torch.Tensor, group=None) -> torch.Tensor:
+    """Mean over ranks of the local ``mask.sum()`` (a detached scalar on mask's device): the
+    denominator that makes rank-averaged gradients of ``masked_geom_mse`` equal the global
+    batch's (see ``GradAllReducer``).  World size 1: the local sum."""
+    s = mask.detach().sum().reshape(1).to(torch.float64)
+    if dist.is_available() and dist.is_initialized():
+        dist.all_reduce(s, group=group)
+        s = s / dist.get_world_size(group)
+    return s.to(mask.dtype).reshape(())
+
+
 class GradAllReducer:
     """Data-parallel gradient averaging for the training step (train_latent_cond.py:136-163 run
     on every rank with its own batch).
 
-    After ``loss.backward()`` each rank holds dLoss_r/dθ of its local mean loss; ``reduce()``
-    replaces every ``p.grad`` with the mean over ranks, which is the gradient of the global-batch
-    mean loss when the local batches have equal sizes (the single-process reference trained on
-    the concatenated batch gives the same gradient up to fp32 summation order).  Then every rank
+    After ``loss.backward()`` each rank holds dLoss_r/dθ of its local loss; ``reduce()``
+    replaces every ``p.grad`` with the mean over ranks.  For the per-sample mean terms of the
+    training loss (the noise MSE) that is the gradient of the global-batch loss when the local
+    batches have equal sizes (the single-process reference trained on the concatenated batch
+    gives the same gradient up to fp32 summation order).  It is NOT for a term normalised by a
+    data-dependent local count: ``masked_geom_mse`` divides by the rank's own mask sum, and the
+    rank mean of sum_r / mask_r differs from (sum of sums) / (sum of masks) whenever the ranks'
+    mask sums differ.  Pass ``denom=global_mask_mean(geom_mask)`` to ``masked_geom_mse`` (one
+    scalar all-reduce) to normalise the geom term globally; the reduced gradient is then the
+    global batch's.  Then every rank
     applies the same optimizer step to identical parameters (start them identical with
     ``broadcast_module``), so replicas never drift.
 

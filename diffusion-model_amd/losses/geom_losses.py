@@ -7,7 +7,14 @@ import torch
 
 
 def masked_geom_mse(geom_pred: torch.Tensor, geom_gt: torch.Tensor, geom_mask: torch.Tensor,
-                    eps: float = 1e-6) -> torch.Tensor:
-    """sum(mask * (pred - gt)^2) / clamp_min(sum(mask), eps)."""
+                    eps: float = 1e-6, denom: torch.Tensor = None) -> torch.Tensor:
+    """sum(mask * (pred - gt)^2) / clamp_min(sum(mask), eps).
+
+    ``denom`` (extension, default None = the reference's formula): use this mask sum instead of
+    the local one.  Data-parallel training passes ``dmx.distributed.global_mask_mean(geom_mask)``
+    — the mean over ranks of the local mask sums — so that the rank-averaged gradient
+    (``GradAllReducer``) is the gradient of the global batch's masked mean (sum of all ranks'
+    numerators over the sum of all ranks' mask sums)."""
     num = (geom_mask * (geom_pred - geom_gt).pow(2)).sum()
-    return num / geom_mask.sum().clamp_min(eps)
+    d = geom_mask.sum() if denom is None else denom
+    return num / d.clamp_min(eps)

@@ -326,3 +326,36 @@ def test_grad_allreduce_equals_full_batch_mean(fn, world):
                 assert torch.allclose(res[r][n], p.grad, rtol=1e-5, atol=1e-7), n
     for r in range(1, world):
         assert torch.equal(res[0]["l1.weight"], res[r]["l1.weight"])
+
+
+def _geom_batch():
+    g = torch.Generator().manual_seed(5)
+    pred_in = torch.randn((8, 4), generator=g)
+    gt = torch.randn((8, 4), generator=g)
+    mask = (torch.rand((8, 4), generator=g) < torch.linspace(0.1, 0.9, 8)[:, None]).float()
+    return pred_in, gt, mask
+
+
+def _dp_geom(rank, world):
+    from losses.geom_losses import masked_geom_mse
+    w = torch.nn.Parameter(torch.linspace(-1.0, 1.0, 4))
+    x, gt, mask = _geom_batch()
+    s, e = dd.shard_range(8, world, rank)
+    loss = masked_geom_mse(x[s:e] * w, gt[s:e], mask[s:e], denom=dd.global_mask_mean(mask[s:e]))
+    loss.backward()
+    dd.GradAllReducer([w]).reduce()
+    return w.grad.clone()
+
+
+def test_grad_allreduce_masked_geom_global_denominator():
+    """masked_geom_mse with the all-reduced mask denominator: the rank-averaged gradient equals
+    the single-process gradient of the whole batch's masked mean although the two shards' mask
+    sums differ (the reference's local denominator would not)."""
+    from losses.geom_losses import masked_geom_mse
+    res = run(_dp_geom, 2)
+    w = torch.nn.Parameter(torch.linspace(-1.0, 1.0, 4))
+    x, gt, mask = _geom_batch()
+    assert mask[:4].sum() != mask[4:].sum()
+    masked_geom_mse(x * w, gt, mask).backward()
+    for r in range(2):
+        assert torch.allclose(res[r], w.grad, rtol=1e-5, atol=1e-7)
