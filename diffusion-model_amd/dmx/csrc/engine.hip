@@ -2187,7 +2187,7 @@ int dmx_eval_metrics(const uint8_t* gt, const uint8_t* pred, int n, int h, int w
                      double sigma, int* workspace, double* out, void* stream) {
   return guarded([&] {
     REQUIRE(gt && pred && workspace && out, "null tensor");
-    REQUIRE(n >= 1 && h >= 1 && w >= 1 && w <= 1024, "bad shape (1 <= w <= 1024)");
+    REQUIRE(n >= 1 && h >= 1 && w >= 1 && h <= 16384 && w <= 16384, "bad shape (1 <= h, w <= 16384)");
     REQUIRE((size_t)h * w < ((size_t)1 << 31) && (size_t)h * h + (size_t)w * w < ((size_t)1 << 30), "image too large");
     EvalParams p{gt, pred, h, w, gray, threshold, invert, sigma, workspace, out};
     eval_metrics_kernel<<<n, 256, 0, (hipStream_t)stream>>>(p);

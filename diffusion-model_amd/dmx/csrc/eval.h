@@ -7,9 +7,11 @@
 // far noise) and 239-272 (compute_metrics).
 //
 // EDT: exact.  Pass 1 (per column) gives the squared vertical distance to the nearest GT pixel
-// of that column; pass 2 (per row) takes min_x' (x - x')^2 + g2(x') over the row (brute force:
-// W <= 1024 here, every pixel's minimum over its row kept in integers), so d2 is the exact
-// integer squared distance and dist = sqrt((double)d2) is scipy's float64 value bit for bit.
+// of that column; pass 2 (per row) takes min_x' (x - x')^2 + g2(x') over the row (brute force,
+// every pixel's minimum over its row kept in integers; the row is staged in LDS up to W = 1024
+// and read from the workspace beyond), so d2 is the exact integer squared distance and
+// dist = sqrt((double)d2) is scipy's float64 value bit for bit.  h, w <= 16384 keeps every
+// finite d2 below EV_INF.
 // An image with no GT pixel: scipy's transform then measures from the virtual feature (-1, 0),
 // d2 = (y + 1)^2 + x^2 (scipy 1.15.3, checked in the oracle tests); reproduced.
 // Sums: counts in 64-bit integers, the weighted hits in double, reduced in a fixed order.
@@ -71,9 +73,12 @@ static __global__ __launch_bounds__(256) void eval_metrics_kernel(const EvalPara
   const double two_s2 = 2.0 * (p.sigma * p.sigma);
   long long inter = 0, uni = 0, ga = 0, pa = 0, far = 0;
   double wsum = 0.0;
+  const bool staged = W <= 1024;
   for (int y = 0; y < H; ++y) {
-    for (int x = tid; x < W; x += 256) row[x] = g2[(size_t)y * W + x];
+    if (staged)
+      for (int x = tid; x < W; x += 256) row[x] = g2[(size_t)y * W + x];
     __syncthreads();
+    const int* rw = staged ? row : g2 + (size_t)y * W;
     for (int x = tid; x < W; x += 256) {
       int d2;
       if (empty_gt) {
@@ -81,7 +86,7 @@ static __global__ __launch_bounds__(256) void eval_metrics_kernel(const EvalPara
       } else {
         d2 = EV_INF;
         for (int xx = 0; xx < W; ++xx) {
-          const int dx = x - xx, v = row[xx];
+          const int dx = x - xx, v = rw[xx];
           if (v != EV_INF) d2 = min(d2, dx * dx + v);
         }
       }

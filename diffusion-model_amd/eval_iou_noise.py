@@ -173,10 +173,14 @@ def overdraw_rate(x: np.ndarray, threshold: float = 1.0) -> float:
 
 # ---- the reference's main (eval_iou_noise.py:303-482) as a function ---------------------------
 def evaluate(gt_dir, gen_dir, out_dir, threshold: int = 128, invert: bool = False, sigma: float = 2.0,
-             max_pairs: int = -1, save_diff: bool = False, workers: int = 8) -> pd.DataFrame:
+             max_pairs: int = -1, save_diff: bool = False, workers: int = 8, chunk_pairs: int = 256) -> pd.DataFrame:
     """Pairs p{k}.jpg with pic{k+1}.png, writes the binarised / side-by-side (/ diff) PNGs, the
     per-pair and summary CSVs and config.txt under out_dir/run_<timestamp>, returns the summary.
-    Decoding and PNG writes run on a thread pool; every same-shape group of pairs is one kernel."""
+    Pairs are processed in chunks of ``chunk_pairs`` (bounded host and device memory): decoding
+    and PNG writes run on a thread pool, every same-shape group of a chunk is one kernel launch.
+    ``distance_backend`` in the summary / config.txt reads ``dmx`` (the reference writes
+    ``scipy``): the exact EDT runs in csrc/eval.h and reproduces scipy's float64 distances bit for
+    bit, so every metric column is the reference's."""
     gt_dir, gen_dir, out_root = Path(gt_dir), Path(gen_dir), Path(out_dir)
     out_root.mkdir(parents=True, exist_ok=True)
     if not gt_dir.exists():
@@ -203,36 +207,43 @@ def evaluate(gt_dir, gen_dir, out_dir, threshold: int = 128, invert: bool = Fals
     if not pairs:
         raise RuntimeError("有効な比較ペアが見つかりません。\n正解: p00000.jpg, p00001.jpg...\n"
                            "生成: pic1.png, pic2.png...\n対応: p00000 <-> pic1, p00001 <-> pic2 ...\n")
+    rows: List[dict] = []
     with ThreadPoolExecutor(max_workers=workers) as pool:
-        grays = list(pool.map(lambda pr: (load_gray(pr[1]), load_gray(pr[2])), pairs))
-        masks = [((g < threshold) if invert else (g >= threshold), (q < threshold) if invert else (q >= threshold))
-                 for g, q in grays]
-        metrics: List[Dict[str, float]] = [None] * len(pairs)  # type: ignore
-        groups: Dict[tuple, List[int]] = {}
-        for i, (g, q) in enumerate(masks):
-            _check_pair(g, q)
-            groups.setdefault(g.shape, []).append(i)
-        for idx in groups.values():
-            for i, m in zip(idx, compute_metrics_batch([masks[i][0] for i in idx], [masks[i][1] for i in idx], sigma)):
-                metrics[i] = m
-        rows, jobs = [], []
-        for (gt_idx, gt_path, gen_path), (gm, pm), m in zip(pairs, masks, metrics):
-            gt_bin = bin_gt_dir / f"{gt_path.stem}_bin.png"
-            gen_bin = bin_gen_dir / f"{gen_path.stem}_bin.png"
-            pair_path = bin_pair_dir / f"pair_gt{gt_idx:05d}_vs_{gen_path.stem}.png"
-            jobs.append(pool.submit(lambda a, b: mask_to_pil(a).save(b), gm, gt_bin))
-            jobs.append(pool.submit(lambda a, b: mask_to_pil(a).save(b), pm, gen_bin))
-            jobs.append(pool.submit(save_side_by_side, gm, pm, pair_path))
-            diff_path = None
-            if save_diff:
-                diff_path = diff_dir / f"diff_gt{gt_idx:05d}_vs_{gen_path.stem}.png"
-                jobs.append(pool.submit(save_diff_visual, gm, pm, diff_path))
-            rows.append({"gt_index": gt_idx, "gt_file": gt_path.name, "gen_file": gen_path.name,
-                         "gt_bin": str(gt_bin.relative_to(run_dir)), "gen_bin": str(gen_bin.relative_to(run_dir)),
-                         "pair_bin": str(pair_path.relative_to(run_dir)),
-                         "diff_bin": str(diff_path.relative_to(run_dir)) if diff_path is not None else "", **m})
-        for j in jobs:
-            j.result()
+        # bounded chunks of pairs: host memory holds at most `chunk_pairs` decoded pairs (the
+        # reference holds one); each same-shape group of a chunk is one kernel launch
+        for c0 in range(0, len(pairs), max(1, int(chunk_pairs))):
+            chunk = pairs[c0:c0 + max(1, int(chunk_pairs))]
+            grays = list(pool.map(lambda pr: (load_gray(pr[1]), load_gray(pr[2])), chunk))
+            masks = [((g < threshold) if invert else (g >= threshold), (q < threshold) if invert else (q >= threshold))
+                     for g, q in grays]
+            del grays
+            metrics: List[Dict[str, float]] = [None] * len(chunk)  # type: ignore
+            groups: Dict[tuple, List[int]] = {}
+            for i, (g, q) in enumerate(masks):
+                _check_pair(g, q)
+                groups.setdefault(g.shape, []).append(i)
+            for idx in groups.values():
+                for i, m in zip(idx, compute_metrics_batch([masks[i][0] for i in idx], [masks[i][1] for i in idx],
+                                                           sigma)):
+                    metrics[i] = m
+            jobs = []
+            for (gt_idx, gt_path, gen_path), (gm, pm), m in zip(chunk, masks, metrics):
+                gt_bin = bin_gt_dir / f"{gt_path.stem}_bin.png"
+                gen_bin = bin_gen_dir / f"{gen_path.stem}_bin.png"
+                pair_path = bin_pair_dir / f"pair_gt{gt_idx:05d}_vs_{gen_path.stem}.png"
+                jobs.append(pool.submit(lambda a, b: mask_to_pil(a).save(b), gm, gt_bin))
+                jobs.append(pool.submit(lambda a, b: mask_to_pil(a).save(b), pm, gen_bin))
+                jobs.append(pool.submit(save_side_by_side, gm, pm, pair_path))
+                diff_path = None
+                if save_diff:
+                    diff_path = diff_dir / f"diff_gt{gt_idx:05d}_vs_{gen_path.stem}.png"
+                    jobs.append(pool.submit(save_diff_visual, gm, pm, diff_path))
+                rows.append({"gt_index": gt_idx, "gt_file": gt_path.name, "gen_file": gen_path.name,
+                             "gt_bin": str(gt_bin.relative_to(run_dir)), "gen_bin": str(gen_bin.relative_to(run_dir)),
+                             "pair_bin": str(pair_path.relative_to(run_dir)),
+                             "diff_bin": str(diff_path.relative_to(run_dir)) if diff_path is not None else "", **m})
+            for j in jobs:
+                j.result()
     df = pd.DataFrame(rows)
     iou_mean, iou_std = mean_std(df["iou"].to_numpy(dtype=np.float64))
     gt_iou_mean, gt_iou_std = mean_std(df["gt_iou"].to_numpy(dtype=np.float64))

@@ -161,7 +161,7 @@ int dmx_latent_frames_u8(const float* z, uint8_t* out, int n, int c, int h, int 
 /* ---- generated-image metrics (replaces eval_iou_noise.py:77-94 binarisation and 162-272
  * distance transform / compute_metrics) ------------------------------
  * gt, pred: (n,h,w) uint8 device — masks (0 / nonzero; gray = 0) or grayscale images binarised
- * here (gray = 1: foreground = v < threshold if invert else v >= threshold); w <= 1024.
+ * here (gray = 1: foreground = v < threshold if invert else v >= threshold); h, w <= 16384.
  * workspace: n*h*w int32 device scratch; out: (n,9) float64 device =
  * {iou, gt_iou, far_noise_ratio, gauss_recall, inter, union, gt_area, pred_area, fp}. */
 int dmx_eval_metrics(const uint8_t* gt, const uint8_t* pred, int n, int h, int w, int gray, int threshold, int invert,

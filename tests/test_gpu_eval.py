@@ -53,6 +53,20 @@ def test_random_masks_vs_oracle(cuda):
         _check([r[k] for k in KEYS], [e[k] for k in KEYS])
 
 
+def test_wide_masks_vs_oracle(cuda):
+    """w > 1024: pass 2 reads the row from the workspace instead of LDS (same exact EDT)."""
+    import eval_iou_noise as ev
+    from oracle import eval_ref
+    rng = np.random.default_rng(9)
+    gts = rng.random((2, 12, 1500)) < 0.01
+    preds = rng.random((2, 12, 1500)) < 0.02
+    gts[1] = False  # no GT pixel: scipy's virtual-feature distances
+    got = ev.compute_metrics_batch(list(gts), list(preds), sigma=2.0)
+    for r, gm, pm in zip(got, gts, preds):
+        e = eval_ref.compute_metrics(gm, pm, 2.0)
+        _check([r[k] for k in KEYS], [e[k] for k in KEYS])
+
+
 def test_errors_like_reference(cuda):
     import eval_iou_noise as ev
     a = np.zeros((8, 8), bool)
@@ -85,3 +99,7 @@ def test_evaluate_directories_end_to_end(golden, cuda, tmp_path):
     assert np.allclose(df[list(KEYS)].to_numpy(), g["metrics"], rtol=1e-12, atol=0)  # through CSV text
     assert int(summary["n_pairs"][0]) == len(g["gt_lens"])
     assert len(os.listdir(os.path.join(run_dir, "diff"))) == len(g["gt_lens"])
+    # bounded chunks (one pair per chunk): the same per-pair rows
+    s1 = ev.evaluate(gt_dir, gen_dir, tmp_path / "out1", threshold=128, invert=True, sigma=2.0, chunk_pairs=1)
+    d1 = pd.read_csv(os.path.join(s1["run_dir"][0], "metrics_detail.csv"))
+    assert d1[list(KEYS)].equals(df[list(KEYS)])

@@ -73,6 +73,52 @@ def test_native_step_matches_reference_and_oracle(cuda, tag):
     assert worst[0][0] <= 1e-4, worst[:5]
 
 
+def test_native_grads_at_bench_shape_vs_oracle(cuda):
+    """The bench.py training leg's shape: B = 32 latents of 28 x 28 (224^2 images through the VAE),
+    t ~ U{1..1000}, CFG dropout (label 0 and zeroed conditions on dropped rows), geom_lambda 0.5
+    — the wgrad split counts, two-pass colsums, GroupNorm-backward chunking and attention lengths
+    of the reported training throughput — every gradient within 1e-4 rel-L2 of the oracle."""
+    from losses.geom_losses import masked_geom_mse
+    from oracle import train_ref
+    from dmx import synth
+    B, hw = 32, 28
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn((B, 4, hw, hw), generator=g)
+    t = torch.randint(1, 1001, (B,), generator=g)
+    classes = torch.randint(1, 4, (B,), generator=g)
+    drop = torch.rand(B, generator=g) < 0.1
+    drop[:2] = True
+    y = torch.where(drop, torch.zeros_like(classes), classes)
+    keep = (~drop).float().unsqueeze(1)
+    vals = torch.rand((B, 12), generator=g) * keep
+    mask = (torch.rand((B, 12), generator=g) > 0.3).float() * keep
+    noise = torch.randn((B, 4, hw, hw), generator=g)
+    gt = torch.rand((B, 12), generator=g)
+    sd = synth.unet_cond_geom_weights(0)
+    from models.unet_cond_geom import UnetCondWithGeomHead
+    m = UnetCondWithGeomHead()
+    m.load_state_dict(sd)
+    m.to(cuda).train()
+    dv = [v.to(cuda) for v in (x, t, y, vals, mask, noise, gt)]
+    eps, gp = m(dv[0], dv[1], dv[2], cond_vals=dv[3], cond_mask=dv[4])
+    loss = F.mse_loss(eps, dv[5]) + 0.5 * masked_geom_mse(gp, dv[6], dv[4])
+    m.zero_grad(set_to_none=True)
+    loss.backward()
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    rloss, _, _, ref = train_ref.loss_and_grads(sd, x, t, y, vals, mask, noise, gt, mask, 0.5, True, False)
+    assert abs(float(loss) - float(rloss)) <= 2e-5 * float(rloss)
+    worst = []
+    for n, p in m.named_parameters():
+        if ref[n] is None:
+            assert p.grad is None, n
+            continue
+        a, b = p.grad.detach().double().cpu(), ref[n].double()
+        worst.append((float((a - b).norm() / max(float(b.norm()), 1e-30)), n))
+    worst.sort(reverse=True)
+    print("[train bench shape] worst rel-L2 vs oracle:", worst[:5])
+    assert worst[0][0] <= 1e-4, worst[:5]
+
+
 def test_two_adam_steps_match_reference(cuda):
     tag = "g"
     m, geom = _model(tag, cuda)
