@@ -295,7 +295,8 @@ def train_leg(args, dev, world=1, rank=0):
 
 MFMA_FAMILIES = ("igemm_x3_kernel", "igemm_pp_kernel", "igemm_f32_kernel", "attention_x3_kernel",
                  "attention16_kernel", "attention_kernel", "tok_ln_qkv_kernel", "tok_ln_qkv_lds_kernel",
-                 "tok_attn_out_kernel")
+                 "tok_attn_out_kernel", "igemm_halo_kernel", "igemm_halo_cs_kernel")
+X3_FAMILIES = ("igemm_pp_kernel", "attention16_kernel", "igemm_halo_kernel", "igemm_halo_cs_kernel")
 
 
 def family(name):
@@ -308,7 +309,7 @@ def _entry(fam, a, pmc_fam):
     if fam in MFMA_FAMILIES:
         per_launch = a["flops"] / a["n"]
         achieved = per_launch / (avg_ms * 1e-3) / 1e12
-        if "x3" in fam or fam.startswith("tok_") or fam in ("igemm_pp_kernel", "attention16_kernel"):
+        if "x3" in fam or fam.startswith("tok_") or fam in X3_FAMILIES:
             # fp32 operands as fp16 hi+lo: 3 f16 MFMAs per algorithmic fp32 multiply-add
             peak, mfma = F16_MFMA_PEAK_TFLOPS / 3.0, "f16 x3 split (peak = 2500/3 TF of fp32 work)"
         else:

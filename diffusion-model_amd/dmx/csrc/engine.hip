@@ -819,6 +819,52 @@ static int halo_bn(const Run& R, int src_C, int N, int H, int W, const ConvW& cw
   return 0;
 }
 
+// DMX_HALO_MS (same-box A/B): 0 low-resolution halo conv off (implicit GEMM + split-K); 1 per-tap
+// pipeline only (igemm_halo_kernel MS); 2 chunk-staged BN = 64 kernel (igemm_halo_cs_kernel), the
+// per-tap BN = 128 kernel where that fills 256 blocks (8 x 8, Cout >= 512); 3 (default) chunk-staged
+// everywhere (measured +1.5 % per CFG step over 0, same-box A/B; 1 and 2 in between).
+static int halo_ms_mode() {
+  static const int v = [] {
+    const char* e = std::getenv("DMX_HALO_MS");
+    return e == nullptr ? 3 : std::atoi(e);
+  }();
+  return v;
+}
+static bool halo_ms_enabled() { return halo_ms_mode() != 0; }
+
+// Low-resolution halo conv (igemm_halo.h, W = 8 / 4 square maps): 256-pixel tiles of whole samples,
+// K split over 32-channel chunks until the grid has >= 256 blocks.  Returns the output-channel tile
+// (0: not applicable) and the split count / chunks per split.
+static int halo_ms_bn(const Run& R, int src_C, int N, int H, int W, const ConvW& cw, int epi, bool plain_or_planes,
+                      int* splits, int* cps) {
+  const int Md = (R.tile_n > 0 ? R.tile_n : N) * H * W;
+  const bool x3 = R.m->prec >= 1 && cw.Bh != nullptr;
+  if (!(halo_ms_enabled() && x3 && epi == EPI_STATS && cw.phases == 1 && cw.taps == 9 && H == W &&
+        (W == 8 || W == 4) && src_C % 32 == 0 &&
+        cw.kpad == 9 * src_C && plain_or_planes))
+    return 0;
+  // decisions from Md: a batch not a multiple of 256 / W² samples ends in a partial tile; small
+  // batches all split K into every chunk (the same summation order for a batch and its shards)
+  const int nch = src_C / 32, mt = cdiv(Md, 256);
+  auto plan = [&](int bn, int& sp, int& cp) {
+    const int tiles = mt * (cw.cout / bn);
+    sp = std::max(1, std::min(nch, cdiv(256, tiles)));
+    cp = cdiv(nch, sp);
+    sp = cdiv(nch, cp);
+    return tiles * sp;
+  };
+  int sp = 1, cp = nch, bn = 0;
+  if (halo_ms_mode() != 3 && W == 8 && cw.cout % 128 == 0 && plan(128, sp, cp) >= 256) bn = 128;
+  else if (cw.cout % 64 == 0) {
+    plan(64, sp, cp);
+    bn = 64;
+  }
+  if (bn == 0 || (W == 4 && sp == 1)) return 0;  // W = 4: EPI_PARTIAL instances only
+  *splits = sp;
+  *cps = cp;
+  return bn;
+}
+
 static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, const ConvW& cw, int epi, float* out,
                 const float* res, float2* rowpart, int seg, const _Float16* ash = nullptr,
                 const _Float16* asl = nullptr, Deferred* defer = nullptr, const GnLoad* gn = nullptr) {
@@ -839,10 +885,17 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   const int hbn = halo_bn(R, s.C, N, H, W, cw, epi, ash != nullptr || src_mode == SRC_PLAIN);
   if (gn != nullptr && (hbn == 0 || ash != nullptr || src_mode != SRC_PLAIN))
     throw Error(DMX_E_INTERNAL, "gemm: GroupNorm-on-load needs the halo conv on a plain fp32 source");
+  int ms_splits = 1, ms_cps = 0;
+  const int msbn = hbn ? 0
+                       : halo_ms_bn(R, s.C, N, H, W, cw, epi, ash != nullptr || src_mode == SRC_PLAIN, &ms_splits,
+                                    &ms_cps);
   const int bk = pp ? 32 : x3 ? 64 : IG_BK;
   const int nkt = cw.kpad / bk;
   int splits = 1, ksplit = nkt;
-  if (!hbn && !pp && cw.phases == 1 && blocks < split_below() && nkt * bk >= 512) {  // split K below 2 blocks / CU
+  if (msbn) {  // low-resolution halo conv: K split over channel chunks (ksplit = chunks per split)
+    splits = ms_splits;
+    ksplit = ms_cps;
+  } else if (!hbn && !pp && cw.phases == 1 && blocks < split_below() && nkt * bk >= 512) {  // split K below 2 blocks / CU
     splits = std::min(std::min(8, std::max(2, 512 / blocks)), nkt * bk / 256);
     ksplit = cdiv(nkt, splits);
     splits = cdiv(nkt, ksplit);
@@ -934,6 +987,26 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   auto name_f32 = [&](int e) {
     std::snprintf(nm, sizeof nm, "igemm_f32_kernel<%d, %d, %d, %d>", bm, bn, src_mode, e);
   };
+  if (msbn) {  // low-resolution halo conv: 256-pixel tiles of whole samples (igemm_halo.h MS)
+    const int e = splits > 1 ? (int)EPI_PARTIAL : (int)EPI_STATS;
+    dim3 gm(cdiv(M, 256), cw.cout / msbn, splits);
+    const bool cs = msbn == 64 && halo_ms_mode() >= 2;
+    if (cs) std::snprintf(nm, sizeof nm, "igemm_halo_cs_kernel<%d, %d, %d, %d>", e, sa, x1 ? 1 : 0, W);
+    else std::snprintf(nm, sizeof nm, "igemm_halo_kernel<%d, %d, %d, %d, %d, 0>", msbn, e, sa, x1 ? 1 : 0, W);
+    R.begin(nm, flops, bytes + (splits > 1 ? 4.0 * splits * M * cw.cout : 0.0));
+    if (cs) launch_halo_cs(e, W, sa, x1 ? 1 : 0, xp, gm, R.st);
+    else launch_halo_ms(e, msbn, W, sa, x1 ? 1 : 0, xp, gm, R.st);
+    R.end();
+    HIPCHK(hipGetLastError());
+    if (splits == 1 || (defer != nullptr && defer->fused)) return rrows;
+    SplitkParams q{partial, splits, M, cw.cout, cw.bias, res, out, rowpart, seg, epi};
+    const int rb = cdiv(M * (cw.cout / 4), 256);
+    R.begin("splitk_reduce_kernel", 0.0, 4.0 * (double)(splits + 1) * M * cw.cout);
+    splitk_reduce_kernel<<<rb, 256, 0, R.st>>>(q);
+    R.end();
+    HIPCHK(hipGetLastError());
+    return rrows;
+  }
   if (splits > 1) {
     dim3 grid(cdiv(M, bm), cdiv(cw.cout, bn), splits);
     if (x3) name_x3(EPI_PARTIAL);

@@ -24,6 +24,18 @@
 // LDS (80-byte rows, conflict-free ds_read_b128 as in igemm_x3): A 2 x HP x 40 f16 x 2 planes
 // (108.8 KB at W = 32), B 2 x BN x 40 f16 x 2 planes (41 KB at BN = 128): one block per CU, two
 // waves per SIMD.  Waves: 4 (rows) x 2 (columns), 64 x BN/2 each.
+//
+// Low resolution (W = 8, 4; square maps): a 256-pixel tile is 256 / W² WHOLE samples.  Their halos
+// are stacked in one LDS image with the zero borders shared: row pitch W + 1 (the zero column right
+// of image row y is the zero column left of row y + 1), one zero row before every sample and after
+// the last, i.e. sample s row y sits in halo row 1 + s (W + 1) + y.  Every tap (dy, dx) of every
+// output pixel then reads halo slot base + dy (W + 1) + dx, zero exactly where the reference pads.
+// Halo pixels per output pixel: 1.30 (W = 8) / 1.59 (W = 4) instead of the implicit GEMM's 9.
+// The last tile may hold fewer samples (batch not a multiple of 256 / W²): the missing ones stage
+// as zeros and the epilogue drops their rows.
+// Those convs are too small to fill 256 CUs with whole-K tiles, so they split K over channel chunks
+// (EPI_PARTIAL: split z owns chunks [z P.g.ksplit, (z + 1) P.g.ksplit), its partial sums go to slab
+// z, reduced in split order by reduce_norm_kernel / splitk_reduce_kernel like the implicit GEMMs').
 #pragma once
 #include "common.h"
 #include "igemm.h"
@@ -42,9 +54,15 @@ template <int BN, int EPI, int SA, int X1, int W, int GNA = 0, int NWN = 2, int 
 __global__ __launch_bounds__(64 * NWM * NWN) void igemm_halo_kernel(const X3Params P) {
   constexpr int NTH = 64 * NWM * NWN;              // threads: NWM (rows) x NWN (columns) waves
   const IgemmParams& p = P.g;
-  constexpr int TR = 256 / W;                     // output image rows per tile
-  constexpr int HWD = W + 2, HP = (TR + 2) * HWD;  // halo row width / pixels
+  constexpr bool MS = W <= 8;                      // multi-sample tiles (H == W), stacked halos
+  constexpr int TR = 256 / W;                      // output image rows per tile (MS: over the samples)
+  constexpr int SPT = MS ? 256 / (W * W) : 1;      // samples per tile
+  constexpr int HWD = MS ? W + 1 : W + 2;          // halo row pitch
+  constexpr int HP = MS ? (1 + SPT * (W + 1)) * HWD + 1 : (TR + 2) * HWD;  // halo pixels
   constexpr int CK = 32, RS = CK + 8;              // channels per chunk, f16 per LDS row
+  static_assert(!MS || (W == 4 || W == 8), "multi-sample halo tiles: W = 4 or 8");
+  static_assert(!(MS && GNA), "GroupNorm-on-load needs whole-row tiles of one sample");
+  static_assert(EPI == EPI_STATS || EPI == EPI_PARTIAL, "halo epilogues");
   constexpr int WM = 256 / NWM, WN = BN / NWN, TM = WM / 32, TN = WN / 32;
   constexpr int PW = SA ? 8 : 4;                   // channels per staged A piece (16 bytes)
   constexpr int PPR = CK / PW;                     // pieces per halo pixel per plane
@@ -67,6 +85,10 @@ __global__ __launch_bounds__(64 * NWM * NWN) void igemm_halo_kernel(const X3Para
   const int C = p.src.C;
   const int nsmp = m0 / HW, y0 = (m0 - nsmp * HW) / W;  // tile = rows y0 .. y0 + TR - 1 of sample nsmp
   constexpr int AES = SA ? 2 : 4;
+  // channel chunks of this block: all of them, or split bz's range (EPI_PARTIAL)
+  const int nch_all = C / CK;
+  const int cbeg = EPI == EPI_PARTIAL ? bz * p.ksplit : 0;
+  const int nch = EPI == EPI_PARTIAL ? min(p.ksplit, nch_all - cbeg) : nch_all;
 
   // halo pieces of this thread: element offset of channel 0 of the piece (chunk 0), or -1 (zero)
   int hoff[NPI];
@@ -78,9 +100,18 @@ __global__ __launch_bounds__(64 * NWM * NWN) void igemm_halo_kernel(const X3Para
     hpix[i] = (short)h;
     hq[i] = (short)q;
     const int hy = h / HWD, hx = h - hy * HWD;
-    const int y = y0 + hy - 1, x = hx - 1;
-    const bool ok = e < HP * PPR && y >= 0 && y < p.H && x >= 0 && x < W;
-    hoff[i] = ok ? (((nsmp * p.H + y) * W + x) * C + q * PW) : -1;
+    bool ok;
+    int pix;
+    if constexpr (MS) {  // halo row hy = 1 + s (W + 1) + y (y = W: the zero row after sample s)
+      const int s = (hy - 1) / (W + 1), y = hy - 1 - s * (W + 1), x = hx - 1;
+      ok = e < HP * PPR && hy >= 1 && hy < 1 + SPT * (W + 1) && y < W && x >= 0 && nsmp + s < p.M / HW;
+      pix = ((nsmp + s) * W + y) * W + x;
+    } else {
+      const int y = y0 + hy - 1, x = hx - 1;
+      ok = e < HP * PPR && y >= 0 && y < p.H && x >= 0 && x < W;
+      pix = (nsmp * p.H + y) * W + x;
+    }
+    hoff[i] = ok ? (pix * C + (cbeg * CK + q * PW)) : -1;
   }
   const __amdgpu_buffer_rsrc_t rAh = rsrc_of(SA ? (const void*)P.Ash : (const void*)p.src.src0, P.a_bytes);
   const __amdgpu_buffer_rsrc_t rAl = rsrc_of(SA ? (const void*)P.Asl : (const void*)p.src.src0, P.a_bytes);
@@ -146,7 +177,7 @@ __global__ __launch_bounds__(64 * NWM * NWN) void igemm_halo_kernel(const X3Para
   };
   // pieces [i0, i1) of the staged halo to LDS buffer `buf` (chunk cc)
   auto store_halo = [&](int buf, int cc, int i0, int i1) __attribute__((always_inline)) {
-    const int cst = cc * CK;  // first channel of the chunk (GroupNorm affine)
+    const int cst = (cbeg + cc) * CK;  // first channel of the chunk (GroupNorm affine)
     (void)cst;
 #pragma unroll
     for (int i = 0; i < NPI; ++i) {
@@ -178,11 +209,12 @@ __global__ __launch_bounds__(64 * NWM * NWN) void igemm_halo_kernel(const X3Para
       }
     }
   };
-  // B slice of step s = 9 c + t: k = t * C + c * CK .. + CK of the [Npad][Kpad] planes
+  // B slice of step s = 9 c + t (c: chunk of this block): k = t * C + (cbeg + c) * CK .. + CK of the
+  // [Npad][Kpad] planes
   auto load_b = [&](int s, int set) {
     if (bact) {
       const int c = s / 9, t = s - 9 * c;
-      const int soff = (t * C + c * CK) * 2;
+      const int soff = (t * C + (cbeg + c) * CK) * 2;
       rbh[set] = bload_h8(rBh, boffs, soff);
       if constexpr (!X1) rbl[set] = bload_h8(rBl, boffs, soff);
     }
@@ -215,8 +247,13 @@ __global__ __launch_bounds__(64 * NWM * NWN) void igemm_halo_kernel(const X3Para
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int r = wm * WM + i * 32 + fp;
-    const int ly = r / W, lx = r - ly * W;
-    abase[i] = (ly + 1) * HWD + lx + 1;
+    if constexpr (MS) {  // tile pixel r = sample r / W², row ly, column lx
+      const int s = r / (W * W), ly = (r - s * W * W) / W, lx = r % W;
+      abase[i] = (1 + s * (W + 1) + ly) * HWD + lx + 1;
+    } else {
+      const int ly = r / W, lx = r - ly * W;
+      abase[i] = (ly + 1) * HWD + lx + 1;
+    }
   }
   auto compute = [&](int abuf, int bbuf, int tap) {
     const int ty = (tap * 11) >> 5;  // tap / 3 for tap in [0, 8]
@@ -266,7 +303,6 @@ __global__ __launch_bounds__(64 * NWM * NWN) void igemm_halo_kernel(const X3Para
     }
   };
 
-  const int nch = C / CK;
   const int S = nch * 9;
   // The B slice of step s is loaded at the start of step s - 2 (register set s & 1) and written to
   // LDS after the MFMAs of step s - 1; the next chunk's halo is loaded at tap 0 and written after
@@ -306,6 +342,183 @@ __global__ __launch_bounds__(64 * NWM * NWN) void igemm_halo_kernel(const X3Para
                                              wn & 1, fr, fh);
 }
 
+
+// ---------------------------------------------------------------------------
+// Low-resolution halo conv, chunk-staged (W = 8 / 4, BN = 64, 16 waves of 32 x 32).  The 4 x 4 and
+// 8 x 8 convs give a block only one to four 32-channel chunks (split-K), i.e. 9 - 36 (chunk, tap)
+// steps whose MFMAs (6 per wave) are far shorter than a global-load round trip: with one barrier and
+// a two-step-ahead B load per tap (igemm_halo_kernel) the launch is a chain of load latencies.  Here
+// the B slice of ALL nine taps of a chunk (9 x 64 x 32 f16 per plane, 92 KB for both) sits in LDS
+// beside the chunk's stacked halo (one buffer each): a chunk is one global round trip, issued while
+// the previous chunk's 54 MFMAs per wave run, then barrier, LDS store, barrier.  Same K order (chunk,
+// tap, k16) and MFMA order as igemm_halo_kernel, so the sums are bit-identical to it.
+// ---------------------------------------------------------------------------
+template <int EPI, int SA, int X1, int W>
+__global__ __launch_bounds__(1024) void igemm_halo_cs_kernel(const X3Params P) {
+  constexpr int BN = 64, NTH = 1024;
+  constexpr int SPT = 256 / (W * W), HWD = W + 1, HP = (1 + SPT * (W + 1)) * HWD + 1;
+  constexpr int CK = 32, RS = CK + 8;
+  constexpr int PW = SA ? 8 : 4, PPR = CK / PW, NPI = (HP * PPR + NTH - 1) / NTH;
+  constexpr int BPT = BN * (CK / 8);              // 16-byte B pieces per plane per tap
+  constexpr int NPB = (9 * BPT + NTH - 1) / NTH;  // B pieces per thread per plane per chunk
+  constexpr int AES = SA ? 2 : 4;
+  static_assert(W == 4 || W == 8, "low-resolution maps only");
+  static_assert(EPI == EPI_STATS || EPI == EPI_PARTIAL, "halo epilogues");
+  constexpr int LA = X1 ? 1 : HP, LB = X1 ? 1 : 9 * BN;
+  __shared__ __attribute__((aligned(16))) _Float16 Ah[HP][RS];
+  __shared__ __attribute__((aligned(16))) _Float16 Al[LA][RS];
+  __shared__ __attribute__((aligned(16))) _Float16 Bhs[9 * BN][RS];
+  __shared__ __attribute__((aligned(16))) _Float16 Bls[LB][RS];
+
+  const IgemmParams& p = P.g;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  int mt, nt, bz;
+  xcd_tile(mt, nt, bz);
+  const int m0 = mt * 256, n0 = nt * BN;
+  const int HW = W * W, C = p.src.C;
+  const int nsmp = m0 / HW, nsamp = p.M / HW;
+  const int nch_all = C / CK;
+  const int cbeg = EPI == EPI_PARTIAL ? bz * p.ksplit : 0;
+  const int nch = EPI == EPI_PARTIAL ? min(p.ksplit, nch_all - cbeg) : nch_all;
+
+  // halo pieces (stacked samples, as igemm_halo_kernel MS): element offset of the piece's first
+  // channel in chunk 0 of this block, or -1 (zero)
+  int hoff[NPI];
+  short hpix[NPI], hq[NPI];
+#pragma unroll
+  for (int i = 0; i < NPI; ++i) {
+    const int e = tid + NTH * i;
+    const int h = e / PPR, q = e - h * PPR;
+    hpix[i] = (short)h;
+    hq[i] = (short)q;
+    const int hy = h / HWD, hx = h - hy * HWD;
+    const int s = (hy - 1) / (W + 1), y = hy - 1 - s * (W + 1), x = hx - 1;
+    const bool ok = e < HP * PPR && hy >= 1 && hy < 1 + SPT * (W + 1) && y < W && x >= 0 && nsmp + s < nsamp;
+    hoff[i] = ok ? ((((nsmp + s) * W + y) * W + x) * C + cbeg * CK + q * PW) : -1;
+  }
+  // B pieces: e -> tap t = e / BPT, column row (e % BPT) / 4, 8-channel quarter e % 4
+  int boff[NPB];
+  short bsl[NPB];  // LDS row t * BN + row (quarter in the low 2 bits), -1: none
+#pragma unroll
+  for (int i = 0; i < NPB; ++i) {
+    const int e = tid + NTH * i;
+    const int t = e / BPT, r = e - t * BPT, row = r >> 2, q = r & 3;
+    const bool ok = e < 9 * BPT;
+    boff[i] = ok ? ((n0 + row) * p.Kpad + t * C + cbeg * CK + q * 8) * 2 : kOOB;
+    bsl[i] = ok ? (short)(((t * BN + row) << 2) | q) : (short)-1;
+  }
+  const __amdgpu_buffer_rsrc_t rAh = rsrc_of(SA ? (const void*)P.Ash : (const void*)p.src.src0, P.a_bytes);
+  const __amdgpu_buffer_rsrc_t rAl = rsrc_of(SA ? (const void*)P.Asl : (const void*)p.src.src0, P.a_bytes);
+  const __amdgpu_buffer_rsrc_t rBh = rsrc_of(P.Bh, P.b_bytes), rBl = rsrc_of(P.Bl, P.b_bytes);
+
+  floatx4 ha4[SA ? 1 : NPI];
+  half8 hah[SA ? NPI : 1], hal[SA ? NPI : 1];
+  half8 rbh[NPB], rbl[NPB];
+  auto load_chunk = [&](int c) {  // c: chunk of this block
+#pragma unroll
+    for (int i = 0; i < NPB; ++i) {
+      rbh[i] = bload_h8(rBh, boff[i], c * CK * 2);
+      if constexpr (!X1) rbl[i] = bload_h8(rBl, boff[i], c * CK * 2);
+    }
+#pragma unroll
+    for (int i = 0; i < NPI; ++i) {
+      const int off = hoff[i] >= 0 ? (hoff[i] + c * CK) * AES : kOOB;
+      if constexpr (SA) {
+        hah[i] = bload_h8(rAh, off, 0);
+        if constexpr (!X1) hal[i] = bload_h8(rAl, off, 0);
+      } else {
+        ha4[i] = bload_f4(rAh, off, 0);
+      }
+    }
+  };
+  auto store_chunk = [&]() {
+#pragma unroll
+    for (int i = 0; i < NPB; ++i) {
+      if (bsl[i] < 0) continue;
+      const int row = bsl[i] >> 2, q = bsl[i] & 3;
+      *reinterpret_cast<half8*>(&Bhs[row][q * 8]) = rbh[i];
+      if constexpr (!X1) *reinterpret_cast<half8*>(&Bls[row][q * 8]) = rbl[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NPI; ++i) {
+      if (tid + NTH * i >= HP * PPR) continue;
+      const int h = hpix[i], q = hq[i];
+      if constexpr (SA) {
+        *reinterpret_cast<half8*>(&Ah[h][q * 8]) = hah[i];
+        if constexpr (!X1) *reinterpret_cast<half8*>(&Al[h][q * 8]) = hal[i];
+      } else if constexpr (X1) {
+        *reinterpret_cast<half4*>(&Ah[h][q * 4]) = __builtin_convertvector(ha4[i], half4);
+      } else {
+        half4 hh, ll;
+        split4(ha4[i], hh, ll);
+        *reinterpret_cast<half4*>(&Ah[h][q * 4]) = hh;
+        *reinterpret_cast<half4*>(&Al[h][q * 4]) = ll;
+      }
+    }
+  };
+
+  const int fr = lane & 31, fh = lane >> 5;
+  int abase;
+  {
+    const int r = wm * 32 + fr;  // tile pixel of this lane's fragment row
+    const int s = r / HW, ly = (r - s * HW) / W, lx = r % W;
+    abase = (1 + s * (W + 1) + ly) * HWD + lx + 1;
+  }
+  const int bcol = wn * 32 + fr;
+  floatx16 acc[1][1];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[0][0][r] = 0.f;
+  // 18 k16 steps per chunk (tap kk / 2, half kk % 2), fragments read one step ahead
+  half8 fa[2], fal[2], fb[2], fbl[2];
+  auto ldf = [&](int kk, int d) {
+    const int t = kk >> 1, s = kk & 1;
+    const int ty = (t * 11) >> 5;  // t / 3
+    const int row = abase + (ty - 1) * HWD + (t - 3 * ty - 1);
+    fa[d] = *reinterpret_cast<const half8*>(&Ah[row][16 * s + 8 * fh]);
+    if constexpr (!X1) fal[d] = *reinterpret_cast<const half8*>(&Al[row][16 * s + 8 * fh]);
+    fb[d] = *reinterpret_cast<const half8*>(&Bhs[t * BN + bcol][16 * s + 8 * fh]);
+    if constexpr (!X1) fbl[d] = *reinterpret_cast<const half8*>(&Bls[t * BN + bcol][16 * s + 8 * fh]);
+  };
+  constexpr int NR = X1 ? 2 : 4, NM = X1 ? 1 : 3;
+  auto compute_chunk = [&]() {
+    ldf(0, 0);
+#pragma unroll
+    for (int kk = 0; kk < 18; ++kk) {
+      const int d = kk & 1;
+      if (kk + 1 < 18) ldf(kk + 1, d ^ 1);
+      if constexpr (!X1) {
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fal[d], fb[d], acc[0][0], 0, 0, 0);
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[d], fbl[d], acc[0][0], 0, 0, 0);
+      }
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(fa[d], fb[d], acc[0][0], 0, 0, 0);
+      if (kk + 1 < 18) {
+        __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
+      }
+    }
+  };
+
+#ifndef DMX_DIAG_CS
+#define DMX_DIAG_CS 0  // diagnostic builds only (wrong results): 1 no MFMAs, 2 no stores, 3 no loads
+#endif
+  if (DMX_DIAG_CS != 3) load_chunk(0);
+  store_chunk();
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    if (DMX_DIAG_CS != 3 && c + 1 < nch) load_chunk(c + 1);  // in flight under this chunk's MFMAs
+    if (DMX_DIAG_CS != 1) compute_chunk();
+    if (c + 1 < nch) {
+      __syncthreads();  // every wave done reading chunk c
+      store_chunk();
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[0][0][r] *= P.inv_scale;
+  if (DMX_DIAG_CS == 2 && acc[0][0][0] != 1234.5f) return;
+  igemm_epilogue<64, 64, EPI>(p, acc, 0, m0 + (wm >> 1) * 64, n0, wm & 1, wn, fr, fh);
+}
 
 // The split weight planes ([Npad][Kpad] f16) re-laid out in MFMA-fragment order: the B operand of
 // v_mfma_f32_32x32x16_f16 for columns 32*nb .. +31 and k = 16*kk .. +15 is 64 lanes x 8 f16, lane

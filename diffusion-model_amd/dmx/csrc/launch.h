@@ -35,6 +35,12 @@ void launch_pp(int bn, int sa, int x1, const X3Params& p, dim3 grid, hipStream_t
 // per channel chunk); mode 2: B staged in LDS per step (one barrier per step).
 // gna = 1 (mode 2, sa = 0): GroupNorm + GELU of the raw source applied while staging.
 void launch_halo(int mode, int bn, int w, int sa, int x1, int gna, const X3Params& p, dim3 grid, hipStream_t st);
+// the same kernel on low-resolution maps (w in {8, 4}, H == w): 256-pixel tiles of whole samples;
+// epi EPI_PARTIAL (grid.z = K splits over 32-channel chunks, P.g.ksplit chunks each) or EPI_STATS
+// (w = 8); bn 128 or 64 (w = 4: 64 only); k_halo_ms.hip.
+void launch_halo_ms(int epi, int bn, int w, int sa, int x1, const X3Params& p, dim3 grid, hipStream_t st);
+// chunk-staged variant (igemm_halo_cs_kernel): BN = 64, all nine taps of a chunk's B slice in LDS.
+void launch_halo_cs(int epi, int w, int sa, int x1, const X3Params& p, dim3 grid, hipStream_t st);
 // register-stage depth of the 4-wave EPI_STATS / EPI_PARTIAL instances (1 or 2; DMX_X3_PF)
 inline int x3_prefetch() {
   static const int v = [] {
