@@ -150,37 +150,59 @@ DMX_DEV void tok_rows(const float* src, int ld, int m0, int M, const float* g, c
   }
 }
 
-// acc[j] = A[arow0 .. +32][0, C) . W[nw + 32j .. +32][0, C)^T  (x3 sum, still scaled by 2^e).
-// B fragments come straight from global memory (L2-resident weights) with a PD-step
-// rolling register prefetch.
+// B fragments of one token GEMM in flight: the first PD k16 steps, requested by tok_prime before
+// the GEMM's A operand exists (under the LayerNorm / epilogue phases and their barriers), so the
+// L2 round trip of the weights is off the critical path; tok_gemm_primed consumes them and keeps
+// PD steps in flight (rolling register prefetch).
+template <int C, int NT>
+struct TokB {
+  static constexpr int S = C / 16, PD = S < DMX_TOK_PD ? S : DMX_TOK_PD;
+  half8 h[PD][NT], l[PD][NT];
+};
+
+// fragment-ordered planes: fragment (column block nb, k16 step s) is 1 KB contiguous, lane-major
+// (one coalesced load per wave); otherwise 32 rows x 32 bytes of the [Npad][Kpad] planes
+struct TokBPtr {
+  const _Float16 *wh, *wl;
+  size_t jstride;
+  int sstride;
+};
+DMX_DEV TokBPtr tok_bptr(const TokW& w, int nw, int fr, int fh) {
+  const bool frag = w.fh != nullptr;
+  const int lane = 32 * fh + fr;
+  TokBPtr p;
+  p.wh = frag ? w.fh + (size_t)(nw >> 5) * (w.kpad / 16) * 512 + lane * 8 : w.h + (size_t)(nw + fr) * w.kpad + 8 * fh;
+  p.wl = frag ? w.fl + (size_t)(nw >> 5) * (w.kpad / 16) * 512 + lane * 8 : w.l + (size_t)(nw + fr) * w.kpad + 8 * fh;
+  p.jstride = frag ? (size_t)(w.kpad / 16) * 512 : (size_t)32 * w.kpad;
+  p.sstride = frag ? 512 : 16;
+  return p;
+}
+template <int NT, int X1>
+DMX_DEV void tok_loadb(const TokBPtr& p, int s, half8* h, half8* l) {
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    h[j] = *reinterpret_cast<const half8*>(p.wh + j * p.jstride + p.sstride * s);
+    if constexpr (!X1) l[j] = *reinterpret_cast<const half8*>(p.wl + j * p.jstride + p.sstride * s);
+  }
+}
 template <int C, int NT, int X1 = 0>
-DMX_DEV void tok_gemm(const _Float16 (*Ah)[C + 8], const _Float16 (*Al)[C + 8], const TokW& w, int nw,
-                      floatx16 (&acc)[NT], int arow0, int fr, int fh) {
-  constexpr int S = C / 16, PD = S < DMX_TOK_PD ? S : DMX_TOK_PD;
+DMX_DEV void tok_prime(const TokW& w, int nw, int fr, int fh, TokB<C, NT>& b) {
+  const TokBPtr p = tok_bptr(w, nw, fr, fh);
+#pragma unroll
+  for (int s = 0; s < TokB<C, NT>::PD; ++s) tok_loadb<NT, X1>(p, s, b.h[s], b.l[s]);
+}
+
+// acc[j] = A[arow0 .. +32][0, C) . W[nw + 32j .. +32][0, C)^T  (x3 sum, still scaled by 2^e),
+// B fragments primed by tok_prime (same w, nw).
+template <int C, int NT, int X1 = 0>
+DMX_DEV void tok_gemm_primed(const _Float16 (*Ah)[C + 8], const _Float16 (*Al)[C + 8], const TokW& w, int nw,
+                             TokB<C, NT>& b, floatx16 (&acc)[NT], int arow0, int fr, int fh) {
+  constexpr int S = C / 16, PD = TokB<C, NT>::PD;
 #pragma unroll
   for (int j = 0; j < NT; ++j)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-  // fragment-ordered planes: fragment (column block nb, k16 step s) is 1 KB contiguous, lane-major
-  // (one coalesced load per wave); otherwise 32 rows x 32 bytes of the [Npad][Kpad] planes
-  const bool frag = w.fh != nullptr;
-  const int lane = 32 * fh + fr;
-  const _Float16* wh = frag ? w.fh + (size_t)(nw >> 5) * (w.kpad / 16) * 512 + lane * 8
-                            : w.h + (size_t)(nw + fr) * w.kpad + 8 * fh;
-  const _Float16* wl = frag ? w.fl + (size_t)(nw >> 5) * (w.kpad / 16) * 512 + lane * 8
-                            : w.l + (size_t)(nw + fr) * w.kpad + 8 * fh;
-  const size_t jstride = frag ? (size_t)(w.kpad / 16) * 512 : (size_t)32 * w.kpad;
-  const int sstride = frag ? 512 : 16;
-  half8 bh[PD][NT], bl[PD][NT];
-  auto loadb = [&](int s, half8* h, half8* l) {
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      h[j] = *reinterpret_cast<const half8*>(wh + j * jstride + sstride * s);
-      if constexpr (!X1) l[j] = *reinterpret_cast<const half8*>(wl + j * jstride + sstride * s);
-    }
-  };
-#pragma unroll
-  for (int s = 0; s < PD; ++s) loadb(s, bh[s], bl[s]);
+  const TokBPtr p = tok_bptr(w, nw, fr, fh);
   const int arow = arow0 + fr;
 #pragma unroll
   for (int s = 0; s < S; ++s) {
@@ -190,10 +212,10 @@ DMX_DEV void tok_gemm(const _Float16 (*Ah)[C + 8], const _Float16 (*Al)[C + 8], 
     half8 ch[NT], cl[NT];
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      ch[j] = bh[s % PD][j];
-      cl[j] = bl[s % PD][j];
+      ch[j] = b.h[s % PD][j];
+      cl[j] = b.l[s % PD][j];
     }
-    if (s + PD < S) loadb(s + PD, bh[s % PD], bl[s % PD]);
+    if (s + PD < S) tok_loadb<NT, X1>(p, s + PD, b.h[s % PD], b.l[s % PD]);
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       if constexpr (!X1) {
@@ -203,6 +225,15 @@ DMX_DEV void tok_gemm(const _Float16 (*Ah)[C + 8], const _Float16 (*Al)[C + 8], 
       acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ch[j], acc[j], 0, 0, 0);
     }
   }
+}
+
+// Unprimed form: B fragments straight from global memory (L2-resident weights), PD steps ahead.
+template <int C, int NT, int X1 = 0>
+DMX_DEV void tok_gemm(const _Float16 (*Ah)[C + 8], const _Float16 (*Al)[C + 8], const TokW& w, int nw,
+                      floatx16 (&acc)[NT], int arow0, int fr, int fh) {
+  TokB<C, NT> b;
+  tok_prime<C, NT, X1>(w, nw, fr, fh, b);
+  tok_gemm_primed<C, NT, X1>(Ah, Al, w, nw, b, acc, arow0, fr, fh);
 }
 
 // Row of accumulator register r inside a wave's 32-row tile (v_mfma_f32_32x32x16 layout).
@@ -217,11 +248,13 @@ __global__ __launch_bounds__(256) void tok_ln_qkv_kernel(const TokParams P) {
   __shared__ __attribute__((aligned(16))) _Float16 Al[64][C + 8];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, fr = lane & 31, fh = lane >> 5;
   const int wm = wid >> 1, wn = wid & 1, m0 = blockIdx.x * 64;
+  const int nw = blockIdx.y * NB + wn * (NB / 2);
+  TokB<C, NT> b;
+  tok_prime<C, NT, X1>(P.w0, nw, fr, fh, b);  // weights in flight with the token loads
   tok_rows<C, 64, ROWS_LN>(P.x, C, m0, P.M, P.l1w, P.l1b, Ah, Al, nullptr, nullptr);
   __syncthreads();
-  const int nw = blockIdx.y * NB + wn * (NB / 2);
   floatx16 acc[NT];
-  tok_gemm<C, NT, X1>(Ah, Al, P.w0, nw, acc, wm * 32, fr, fh);
+  tok_gemm_primed<C, NT, X1>(Ah, Al, P.w0, nw, b, acc, wm * 32, fr, fh);
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     const int col = nw + 32 * j + fr;
@@ -335,10 +368,19 @@ __global__ __launch_bounds__(NW * 64) void tok_attn_out_kernel(const TokParams P
       if constexpr (!X1) *reinterpret_cast<half8*>(&Wl[w][r][q * 8]) = *reinterpret_cast<const half8*>(tw.l + o);
     }
   }
+  // non-WLDS: the next GEMM's first B fragments are requested as soon as the current GEMM has
+  // consumed its own (tok_prime), i.e. before the epilogue / LayerNorm phases and their barriers
+  TokB<C, NT> bf;
+  const TokW* const tws[3] = {&P.w0, &P.w1, &P.w2};
   auto gemm = [&](int w, const TokW& tw, floatx16(&acc)[NT]) {
-    if constexpr (WLDS) tok_gemm_lds<C, NT, X1>(Ah, Al, Wh[w], Wl[X1 ? 0 : w], nw, acc, arow0, fr, fh);
-    else tok_gemm<C, NT, X1>(Ah, Al, tw, nw, acc, arow0, fr, fh);
+    if constexpr (WLDS) {
+      tok_gemm_lds<C, NT, X1>(Ah, Al, Wh[w], Wl[X1 ? 0 : w], nw, acc, arow0, fr, fh);
+    } else {
+      tok_gemm_primed<C, NT, X1>(Ah, Al, tw, nw, bf, acc, arow0, fr, fh);
+      if (w < 2) tok_prime<C, NT, X1>(*tws[w + 1], nw, fr, fh, bf);
+    }
   };
+  if constexpr (!WLDS) tok_prime<C, NT, X1>(P.w0, nw, fr, fh, bf);
 
   for (int t = 0; t < TPB; ++t) {
     const int m0 = (blockIdx.x * TPB + t) * TM;
@@ -396,7 +438,12 @@ __global__ __launch_bounds__(NW * 64) void tok_attn_out_kernel(const TokParams P
         if (m < M) P.out[(size_t)m * C + col] = (acc[j][r] * P.w2.inv_scale + b) + Av[row][col];
       }
     }
-    if (TPB > 1) __syncthreads();  // the next tile overwrites the planes and Av
+    if (TPB > 1) {
+      if constexpr (!WLDS) {
+        if ((blockIdx.x * TPB + t + 1) * TM < M) tok_prime<C, NT, X1>(P.w0, nw, fr, fh, bf);
+      }
+      __syncthreads();  // the next tile overwrites the planes and Av
+    }
   }
 }
 
