@@ -14,7 +14,42 @@ namespace dmx {
 // Exact (erf) GELU and SiLU in fp32, matching the reference's nn.GELU() /
 // F.gelu default (approximate='none') and nn.SiLU (models/unet_cond.py:21,28,63).
 // ---------------------------------------------------------------------------
-DMX_DEV float gelu(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f)); }
+// GELU = x Phi(x), Phi(x) = erfc(-x / sqrt 2) / 2, with erfc(z) = t exp(-z^2 + P(t)), t = 1 / (1 + z / 2)
+// for z = |x| / sqrt 2 >= 0 (the classic erfcc Chebyshev fit, fractional error < 1.2e-7): 17 VALU
+// operations instead of erff's two-branch ~35, which the GroupNorm-on-load convs pay per staged
+// element.  Absolute error <= 2.1e-7 on [0, 3], <= 8.2e-8 on [-3, 0] and <= 3.9e-7 above — the size of
+// the reference's own fp32 rounding of 0.5 x (1 + erf(x / sqrt 2)) (<= 2.5e-7 / 4.7e-8 / 4.5e-7 there),
+// and far more accurate than that form in the negative tail, where it cancels.  Every GELU of the
+// inference path uses this one function, so fused and unfused paths stay bit-identical.
+// The exact-fp32 mode (precision 0: the training forward, the fp32 reference mode) keeps the erf
+// form (gelu_exact; kernels shared by both modes select it with a uniform flag): the training
+// gradients are pinned to the reference's autograd at 1e-4, which the fit's bias does not meet at
+// the bench shape.  DMX_GELU_FAST=0 builds the erff form everywhere (same-box A/B).
+#ifndef DMX_GELU_FAST
+#define DMX_GELU_FAST 1
+#endif
+DMX_DEV float gelu_exact(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f)); }
+DMX_DEV float gelu(float x) {
+#if DMX_GELU_FAST
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, z, 1.0f));
+  float p = 0.17087277f;
+  p = fmaf(p, t, -0.82215223f);
+  p = fmaf(p, t, 1.48851587f);
+  p = fmaf(p, t, -1.13520398f);
+  p = fmaf(p, t, 0.27886807f);
+  p = fmaf(p, t, -0.18628806f);
+  p = fmaf(p, t, 0.09678418f);
+  p = fmaf(p, t, 0.37409196f);
+  p = fmaf(p, t, 1.00002368f);
+  p = fmaf(p, t, -1.26551223f);
+  const float e = t * __builtin_amdgcn_exp2f(fmaf(-z, z, p) * 1.44269504088896340736f);  // erfc(z)
+  const float phi = x >= 0.f ? fmaf(-0.5f, e, 1.0f) : 0.5f * e;
+  return x * phi;
+#else
+  return gelu_exact(x);
+#endif
+}
 DMX_DEV float silu(float x) { return x / (1.0f + expf(-x)); }
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));

@@ -938,6 +938,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   p.partial = partial;
   p.rgrp = rgrp;
   p.nphase = cw.phases;
+  p.gexact = R.m->prec == 0 ? 1 : 0;
   if (s.C != cw.cin) throw Error(DMX_E_INTERNAL, "gemm: source channels != weight channels");
   if (x3 && cw.cin < bk) throw Error(DMX_E_INTERNAL, "gemm: x3 path needs Cin >= K-step");
   if (ash != nullptr && !x3) throw Error(DMX_E_INTERNAL, "gemm: f16-plane operand needs the split GEMM");
@@ -999,7 +1000,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
     R.end();
     HIPCHK(hipGetLastError());
     if (splits == 1 || (defer != nullptr && defer->fused)) return rrows;
-    SplitkParams q{partial, splits, M, cw.cout, cw.bias, res, out, rowpart, seg, epi};
+    SplitkParams q{partial, splits, M, cw.cout, cw.bias, res, out, rowpart, seg, epi, R.m->prec == 0 ? 1 : 0};
     const int rb = cdiv(M * (cw.cout / 4), 256);
     R.begin("splitk_reduce_kernel", 0.0, 4.0 * (double)(splits + 1) * M * cw.cout);
     splitk_reduce_kernel<<<rb, 256, 0, R.st>>>(q);
@@ -1017,7 +1018,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
     R.end();
     HIPCHK(hipGetLastError());
     if (defer != nullptr && defer->fused) return rrows;  // the caller's reduce_norm_kernel sums the slabs
-    SplitkParams q{partial, splits, M, cw.cout, cw.bias, res, out, rowpart, seg, epi};
+    SplitkParams q{partial, splits, M, cw.cout, cw.bias, res, out, rowpart, seg, epi, R.m->prec == 0 ? 1 : 0};
     const int rb = cdiv(M * (cw.cout / 4), 256);
     R.begin("splitk_reduce_kernel", 0.0, 4.0 * (double)(splits + 1) * M * cw.cout);
     splitk_reduce_kernel<<<rb, 256, 0, R.st>>>(q);
@@ -1083,6 +1084,7 @@ static void gn_finalize(Run& R, const float2* rowpart, float2* stats, int N, int
 // or precomputed (stats).
 static void norm(Run& R, NormParams np, int N) {
   if (R.plan) return;
+  np.gexact = R.m->prec == 0 ? 1 : 0;
   // ~2048+ blocks in total, 256..1024 float4 per block (chunks are rounded up to 256 in-kernel)
   const int per = np.HW * (np.C / 4);
   const int target = 1024;  // total blocks aimed at for small tensors (measured +0.3 % over 2048)
@@ -1097,6 +1099,7 @@ static void norm(Run& R, NormParams np, int N) {
 // block per source sample; np describes the normalisation exactly as for norm().
 static void reduce_norm(Run& R, const Deferred& d, NormParams np, int n_src_samples) {
   if (R.plan) return;
+  np.gexact = R.m->prec == 0 ? 1 : 0;
   const int kv = cdiv(np.HW * (np.C / 4), 1024);
   const int n_out = np.n_src > 0 ? 2 * n_src_samples : n_src_samples;
   const int kvt = kv <= 1 ? 1 : kv <= 2 ? 2 : kv <= 4 ? 4 : RN_MAXV;

@@ -44,6 +44,7 @@ struct IgemmParams {
   int nphase;         // phases of this GEMM (1, or 4 for ConvT)
   int ksplit;         // EPI_PARTIAL: K-tiles per split (blockIdx.z = split; phases must be 1)
   float* partial;     // EPI_PARTIAL: [splits][M][Cout]
+  int gexact;         // EPI_BIAS_GELU: 1 = erf-form GELU (exact-fp32 mode)
 };
 
 constexpr int IG_BK = 16;
@@ -176,7 +177,7 @@ DMX_DEV void igemm_epilogue(const IgemmParams& p, floatx16 (&acc)[BM / 64][BN / 
           const int col = n0 + wn * WN + j * 32 + fr;
           const bool v = mv && col < p.Cout;
           float val = acc[i][j][r] + bj[j];
-          if constexpr (EPI == EPI_BIAS_GELU) val = gelu(val);
+          if constexpr (EPI == EPI_BIAS_GELU) val = p.gexact ? gelu_exact(val) : gelu(val);
           if constexpr (EPI == EPI_BIAS_RES) {
             if (v) val += p.res[(size_t)m * p.Cout + col];
           }
@@ -236,7 +237,7 @@ DMX_DEV void igemm_epilogue(const IgemmParams& p, floatx16 (&acc)[BM / 64][BN / 
         const int col = n0 + wn * WN + j * 32 + fr;
         const bool v = mv && col < p.Cout;
         float val = acc[i][j][r] + bj[j];
-        if constexpr (EPI == EPI_BIAS_GELU) val = gelu(val);
+        if constexpr (EPI == EPI_BIAS_GELU) val = p.gexact ? gelu_exact(val) : gelu(val);
         if constexpr (EPI == EPI_BIAS_RES) {
           if (v) val += p.res[oidx * p.Cout + col];
         }
@@ -401,6 +402,7 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(const IgemmParams p) {
 struct SplitkParams {
   const float* partial; int splits; int M, Cout;
   const float* bias; const float* res; float* out; float2* rowpart; int seg; int epi;
+  int gexact;  // EPI_BIAS_GELU: erf-form GELU
 };
 
 static __global__ __launch_bounds__(256) void splitk_reduce_kernel(const SplitkParams p) {
@@ -424,7 +426,7 @@ static __global__ __launch_bounds__(256) void splitk_reduce_kernel(const SplitkP
     }
     if (p.epi == EPI_BIAS_GELU) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = gelu(v[j]);
+      for (int j = 0; j < 4; ++j) v[j] = p.gexact ? gelu_exact(v[j]) : gelu(v[j]);
     } else if (p.epi == EPI_BIAS_RES) {
       const floatx4 r = ld4(p.res + m * p.Cout + c);
 #pragma unroll

@@ -150,6 +150,7 @@ struct NormParams {
   const float* gamma; const float* beta;
   int C, G, HW;
   const float* res; int act;
+  int gexact;                      // 1: GELU in the erf form (exact-fp32 mode), 0: gelu()
   const float* emb; int emb_stride; int emb_off;
   int n_src;                       // >0: raw / stats / res of output sample n come from sample n % n_src
   float* out;                      // fp32 output, or null when only the planes are written
@@ -230,11 +231,21 @@ static __global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
       const float2 st = p.rowpart != nullptr ? st_s : p.stats[ns * p.G + c / cpg];
       floatx4 o = cfix ? gn_apply4v(v[k], st, fg, fb, 0) : gn_apply4(v[k], st, p.gamma, p.beta, c, 0);
       if (res != nullptr) {
+        if (p.gexact) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = gelu(r[k][j] + o[j]);
+          for (int j = 0; j < 4; ++j) o[j] = gelu_exact(r[k][j] + o[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = gelu(r[k][j] + o[j]);
+        }
       } else if (p.act) {
+        if (p.gexact) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = gelu(o[j]);
+          for (int j = 0; j < 4; ++j) o[j] = gelu_exact(o[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = gelu(o[j]);
+        }
       }
       if (p.emb != nullptr) {
         const floatx4 e = cfix ? fe : ld4(p.emb + (size_t)n * p.emb_stride + p.emb_off + c);
@@ -352,11 +363,21 @@ __global__ __launch_bounds__(1024) void reduce_norm_kernel(const float* partial,
       floatx4 o = gn_apply4(v[k], st, p.gamma, p.beta, c, 0);
       if (p.res != nullptr) {
         const floatx4 r = ld4(p.res + sbase + (size_t)idx * 4);
+        if (p.gexact) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = gelu(r[j] + o[j]);
+          for (int j = 0; j < 4; ++j) o[j] = gelu_exact(r[j] + o[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = gelu(r[j] + o[j]);
+        }
       } else if (p.act) {
+        if (p.gexact) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) o[j] = gelu(o[j]);
+          for (int j = 0; j < 4; ++j) o[j] = gelu_exact(o[j]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = gelu(o[j]);
+        }
       }
       if (p.emb != nullptr) {
         const floatx4 e = ld4(p.emb + (size_t)n * p.emb_stride + p.emb_off + c);

@@ -484,7 +484,7 @@ static __global__ void gelu_bwd_kernel(const float* d, const float* pre, float* 
     dst[i] = d[i] * gelu_grad(pre[i]);
 }
 static __global__ void gelu_fwd_kernel(const float* x, float* y, size_t n) {
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) y[i] = gelu(x[i]);
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) y[i] = gelu_exact(x[i]);
 }
 static __global__ void add_kernel(float* dst, const float* src, size_t n) {
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) dst[i] += src[i];
