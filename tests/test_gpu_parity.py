@@ -246,6 +246,32 @@ def test_cfg_step_full_batch_vs_oracle(model, cuda, unet_sd, prec):
     assert rel(out, exp) < TOL
 
 
+@pytest.mark.parametrize("B,hw", [(3, 32), (9, 32), (5, 16)])
+def test_cfg_step_ragged_batches_vs_oracle(model, cuda, unet_sd, B, hw):
+    """Batches that are not a multiple of the low-resolution halo convs' whole-sample tiles (16
+    samples of 4 x 4, 4 of 8 x 8: igemm_halo.h MS) — the last tile holds fewer samples, which stage
+    as zeros and whose rows the epilogue drops — and the split-K slab reduction behind them."""
+    import diff
+    d = diff.Diffuser(1000, device=cuda)
+    g = torch.Generator().manual_seed(300 + B)
+    x = torch.randn((B, 4, hw, hw), generator=g)
+    y = torch.tensor([1 + i % 3 for i in range(B)])
+    vals = torch.rand((B, 12), generator=g)
+    mask = (torch.rand((B, 12), generator=g) > 0.5).float()
+    t = torch.full((B,), 333, dtype=torch.long)
+    torch.manual_seed(78)
+    out = d.denoise_cond(model, x.to(cuda), t.to(cuda), y=y.to(cuda), guidance_scale=3.0,
+                         cond_vals=vals.to(cuda), cond_mask=mask.to(cuda))
+    torch.manual_seed(78)
+    noise = torch.randn(x.shape)
+    _, a, ab = ref.schedule(1000)
+    with torch.no_grad():
+        exp = ref.cfg_step(unet_sd, x, t, y, a, ab, 3.0, 0, vals, mask, noise)
+    err = rel(out, exp)
+    print(f"[ragged B={B} {hw}x{hw}] CFG step rel-L2 vs oracle {err:.2e}")
+    assert err < TOL
+
+
 def test_trajectory_T1000_golden(golden, model, vae, cuda, prec):
     """Full T=1000 CFG trajectory (B=2) on the reference's own draws: latents <= 1e-4, pixels +-1."""
     import diff
