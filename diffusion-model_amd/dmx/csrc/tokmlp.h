@@ -72,22 +72,36 @@ DMX_DEV float group_sum(float s) {
 // load instruction covers 16G contiguous bytes of a row); every load of the pass is issued
 // before any is used.  LN = nn.LayerNorm: two-pass mean / biased variance, eps 1e-5, the
 // same per-element expression as layernorm_kernel.
-template <int C, int TM, int MODE, int NW = 4>
-DMX_DEV void tok_rows(const float* src, int ld, int m0, int M, const float* g, const float* b,
-                      _Float16 (*Ah)[C + 8], _Float16 (*Al)[C + 8], float* mu, float* rs, float* o32 = nullptr,
-                      int ldo = 0) {
-  constexpr int G = C / 16, RP = 64 / G, RW = TM / NW, NP = RW / RP;
+// The loaded rows of one tok_rows pass (tok_rows_load), consumed by tok_rows_put: split so a
+// multi-tile block can load tile t + 1 under tile t's GEMMs.
+template <int C, int TM, int NW>
+struct TokRowsV {
+  static constexpr int G = C / 16, RP = 64 / G, RW = TM / NW, NP = RW / RP;
   static_assert(G == 4 || G == 8 || G == 16, "C");
   static_assert(NP >= 1 && RW % RP == 0, "rows per wave");
+  floatx4 v[NP][4];
+};
+template <int C, int TM, int NW = 4>
+DMX_DEV void tok_rows_load(const float* src, int ld, int m0, int M, TokRowsV<C, TM, NW>& rv) {
+  using R = TokRowsV<C, TM, NW>;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int rr = lane / R::G, c0 = 4 * (lane % R::G);
+#pragma unroll
+  for (int p = 0; p < R::NP; ++p) {
+    const int m = min(m0 + wid * R::RW + p * R::RP + rr, M - 1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) rv.v[p][j] = ld4(src + (size_t)m * ld + c0 + 4 * R::G * j);
+  }
+}
+template <int C, int TM, int MODE, int NW = 4>
+DMX_DEV void tok_rows_put(TokRowsV<C, TM, NW>& rv, int m0, int M, const float* g, const float* b,
+                          _Float16 (*Ah)[C + 8], _Float16 (*Al)[C + 8], float* mu, float* rs, float* o32 = nullptr,
+                          int ldo = 0) {
+  using R = TokRowsV<C, TM, NW>;
+  constexpr int G = R::G, RP = R::RP, RW = R::RW, NP = R::NP;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int rr = lane / G, c0 = 4 * (lane % G);
-  floatx4 v[NP][4];
-#pragma unroll
-  for (int p = 0; p < NP; ++p) {
-    const int m = min(m0 + wid * RW + p * RP + rr, M - 1);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) v[p][j] = ld4(src + (size_t)m * ld + c0 + 4 * G * j);
-  }
+  auto& v = rv.v;
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     const int row = wid * RW + p * RP + rr;
@@ -148,6 +162,15 @@ DMX_DEV void tok_rows(const float* src, int ld, int m0, int M, const float* g, c
       }
     }
   }
+}
+
+template <int C, int TM, int MODE, int NW = 4>
+DMX_DEV void tok_rows(const float* src, int ld, int m0, int M, const float* g, const float* b,
+                      _Float16 (*Ah)[C + 8], _Float16 (*Al)[C + 8], float* mu, float* rs, float* o32 = nullptr,
+                      int ldo = 0) {
+  TokRowsV<C, TM, NW> rv;
+  tok_rows_load<C, TM, NW>(src, ld, m0, M, rv);
+  tok_rows_put<C, TM, MODE, NW>(rv, m0, M, g, b, Ah, Al, mu, rs, o32, ldo);
 }
 
 // B fragments of one token GEMM in flight: the first PD k16 steps, requested by tok_prime before
@@ -320,11 +343,14 @@ __global__ __launch_bounds__(256) void tok_ln_qkv_lds_kernel(const TokParams P) 
   float bias[NT];
 #pragma unroll
   for (int j = 0; j < NT; ++j) bias[j] = P.w0.bias[nb0 + nwl + 32 * j + fr];
+  TokRowsV<C, 64, 4> rv;  // token rows of the next tile, loaded under this tile's GEMM
+  if (blockIdx.x * TPB * 64 < P.M) tok_rows_load<C, 64>(P.x, C, blockIdx.x * TPB * 64, P.M, rv);
   for (int t = 0; t < TPB; ++t) {
     const int m0 = (blockIdx.x * TPB + t) * 64;
     if (m0 >= P.M) break;
-    tok_rows<C, 64, ROWS_LN>(P.x, C, m0, P.M, P.l1w, P.l1b, Ah, Al, nullptr, nullptr);
+    tok_rows_put<C, 64, ROWS_LN>(rv, m0, P.M, P.l1w, P.l1b, Ah, Al, nullptr, nullptr);
     __syncthreads();
+    if (t + 1 < TPB && m0 + 64 < P.M) tok_rows_load<C, 64>(P.x, C, m0 + 64, P.M, rv);
     floatx16 acc[NT];
     tok_gemm_lds<C, NT, X1>(Ah, Al, Wh, Wl, nwl, acc, wm * 32, fr, fh);
 #pragma unroll
@@ -382,14 +408,24 @@ __global__ __launch_bounds__(NW * 64) void tok_attn_out_kernel(const TokParams P
   };
   if constexpr (!WLDS) tok_prime<C, NT, X1>(P.w0, nw, fr, fh, bf);
 
+  // ao -> A planes; LN1(x) -> Av (fp32, the residual of the out-projection): both loads in flight
+  // together, no second read of x later; with several tiles per block the next tile's rows are
+  // loaded under this tile's GEMMs
+  TokRowsV<C, TM, NW> rao, rx;
+  if (blockIdx.x * TPB * TM < M) {
+    tok_rows_load<C, TM, NW>(P.ao, C, blockIdx.x * TPB * TM, M, rao);
+    tok_rows_load<C, TM, NW>(P.x, C, blockIdx.x * TPB * TM, M, rx);
+  }
   for (int t = 0; t < TPB; ++t) {
     const int m0 = (blockIdx.x * TPB + t) * TM;
     if (m0 >= M) break;
-    // ao -> A planes; LN1(x) -> Av (fp32, the residual of the out-projection): both loads in
-    // flight together, no second read of x later
-    tok_rows<C, TM, ROWS_SPLIT, NW>(P.ao, C, m0, M, nullptr, nullptr, Ah, Al, nullptr, nullptr);
-    tok_rows<C, TM, ROWS_LNF, NW>(P.x, C, m0, M, P.l1w, P.l1b, Ah, Al, nullptr, nullptr, &Av[0][0], VS);
+    tok_rows_put<C, TM, ROWS_SPLIT, NW>(rao, m0, M, nullptr, nullptr, Ah, Al, nullptr, nullptr);
+    tok_rows_put<C, TM, ROWS_LNF, NW>(rx, m0, M, P.l1w, P.l1b, Ah, Al, nullptr, nullptr, &Av[0][0], VS);
     __syncthreads();
+    if (TPB > 1 && t + 1 < TPB && m0 + TM < M) {
+      tok_rows_load<C, TM, NW>(P.ao, C, m0 + TM, M, rao);
+      tok_rows_load<C, TM, NW>(P.x, C, m0 + TM, M, rx);
+    }
 
     floatx16 acc[NT];
     // av = ao Wo^T + bo + LN1(x)   (models/unet_cond.py:49-50); each Av element is read and
