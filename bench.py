@@ -328,6 +328,25 @@ def _entry(fam, a, pmc_fam):
     return e
 
 
+def _pmc_by_label(pmc, labels):
+    """PMC bytes keyed by bench.py's kernel labels.  rocprofv3 names carry every template argument
+    (wave layout, prefetch depth), the labels only the leading ones: a label takes the PMC entry whose
+    template arguments start with the label's (the mean if several launch configurations match)."""
+    def split(name):
+        fam, _, rest = name.partition("<")
+        return fam, [a.strip() for a in rest.rstrip(">").split(",")] if rest else []
+    out = {}
+    for lab in labels:
+        if lab in pmc:
+            out[lab] = pmc[lab]
+            continue
+        fam, args = split(lab)
+        hits = [v for k, v in pmc.items() if split(k)[0] == fam and split(k)[1][:len(args)] == args]
+        if hits:
+            out[lab] = sum(hits) / len(hits)
+    return out
+
+
 def roofline(records, pmc=None):
     """Dominant kernel = the kernel family (name without template arguments: every tile /
     epilogue instantiation of the implicit-GEMM conv is one kernel) with the largest summed
@@ -336,6 +355,7 @@ def roofline(records, pmc=None):
     event-timed launch duration.  `traffic` = PMC HBM bytes per launch (profiles/pmc_traffic.json,
     averaged over the family's launches in the step) or null."""
     agg, fams = {}, {}
+    pmc = _pmc_by_label(pmc, {r["kernel"] for r in records}) if pmc is not None else None
     for r in records:
         for key, d in ((r["kernel"], agg), (family(r["kernel"]), fams)):
             a = d.setdefault(key, {"ms": 0.0, "flops": 0.0, "bytes": 0.0, "n": 0, "pmc": 0.0, "pmc_ok": True})
