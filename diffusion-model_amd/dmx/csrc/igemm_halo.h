@@ -162,7 +162,18 @@ __global__ __launch_bounds__(64 * NWM * NWN) void igemm_halo_kernel(const X3Para
   half8 hah[SA ? NPI : 1], hal[SA ? NPI : 1];
   const __amdgpu_buffer_rsrc_t rRes = rsrc_of(GNA == 2 ? (const void*)P.gn_res : (const void*)p.src.src0, P.a_bytes);
   half8 rbh[2], rbl[2];
+  // GNA: every piece of this thread has the same 4 channels of a chunk (NTH is a multiple of PPR), so
+  // the GroupNorm affine of the chunk is 2 float4, loaded with the chunk's halo (not at store time)
+  // (not for GNA = 2 at BN = 128: its 8 extra registers would spill at the 128-VGPR cap)
+  static_assert(NTH % PPR == 0, "piece channel");
+  constexpr bool GPRE = GNA == 1 || (GNA == 2 && BN == 64);
+  floatx4 ggam = {0.f, 0.f, 0.f, 0.f}, gbet = {0.f, 0.f, 0.f, 0.f};
   auto load_halo = [&](int c) {
+    if constexpr (GPRE) {
+      const int ch = (cbeg + c) * CK + (tid % PPR) * PW;
+      ggam = ld4(P.gn_gamma + ch);
+      gbet = ld4(P.gn_beta + ch);
+    }
 #pragma unroll
     for (int i = 0; i < NPI; ++i) {
       const int off = hoff[i] >= 0 ? (hoff[i] + c * CK) * AES : kOOB;
@@ -177,8 +188,6 @@ __global__ __launch_bounds__(64 * NWM * NWN) void igemm_halo_kernel(const X3Para
   };
   // pieces [i0, i1) of the staged halo to LDS buffer `buf` (chunk cc)
   auto store_halo = [&](int buf, int cc, int i0, int i1) __attribute__((always_inline)) {
-    const int cst = (cbeg + cc) * CK;  // first channel of the chunk (GroupNorm affine)
-    (void)cst;
 #pragma unroll
     for (int i = 0; i < NPI; ++i) {
       if (i < i0 || i >= i1) continue;
@@ -190,8 +199,12 @@ __global__ __launch_bounds__(64 * NWM * NWN) void igemm_halo_kernel(const X3Para
       } else {
         floatx4 v = ha4[i];
         if constexpr (GNA) {  // GroupNorm (+ residual) + GELU of the raw source; zero padding stays zero
-          const int ch = cst + q * 4;
-          v = gn_apply4v(v, gst, ld4(P.gn_gamma + ch), ld4(P.gn_beta + ch), GNA == 1 ? 1 : 0);
+          if constexpr (GPRE) {
+            v = gn_apply4v(v, gst, ggam, gbet, GNA == 1 ? 1 : 0);
+          } else {
+            const int ch = (cbeg + cc) * CK + q * 4;
+            v = gn_apply4v(v, gst, ld4(P.gn_gamma + ch), ld4(P.gn_beta + ch), GNA == 1 ? 1 : 0);
+          }
           if constexpr (GNA == 2) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) v[j] = gelu(hr4[i][j] + v[j]);
