@@ -745,11 +745,15 @@ static int halo_mode() {
   return v;
 }
 static bool halo_enabled() { return halo_mode() != 0; }
-// Grids with fewer blocks than this split K (DMX_SPLIT_BELOW, same-box A/B; default 512 = 2 / CU).
+// Grids with fewer blocks than this split K (DMX_SPLIT_BELOW, same-box A/B).  256 (one block per CU):
+// since the low-resolution convs moved to the halo kernels (own split rule), this only decides the
+// 16 x 16 convs of the CFG-shared down1 stage (256 blocks): unsplit, their GroupNorm runs as
+// norm_kernel over many blocks instead of reduce_norm_kernel's one block per sample (+0.25 % per CFG
+// step over 512, 3/3 same-box rounds).
 static int split_below() {
   static const int v = [] {
     const char* e = std::getenv("DMX_SPLIT_BELOW");
-    return e == nullptr ? 512 : std::atoi(e);
+    return e == nullptr ? 256 : std::atoi(e);
   }();
   return v;
 }
