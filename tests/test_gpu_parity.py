@@ -286,9 +286,11 @@ def test_trajectory_T1000_golden(golden, model, vae, cuda, prec):
         x = d.denoise_cond(model, x, t, y=y, guidance_scale=3.0, null_label=0, cond_vals=vals, cond_mask=mask)
         if i in (900, 500, 100):
             assert rel(x, g[f"x_{i}"]) < 1e-4, i
-    assert rel(x, g["x_final"]) < 1e-4
+    err = rel(x, g["x_final"])
     u8 = vae.decode_uint8(x).cpu().numpy()
     ok, info = u8_close(u8, g["u8"])
+    print(f"[trajectory T=1000 {prec}] final latents rel-L2 vs reference {err:.2e}, pixels {info}")
+    assert err < 1e-4
     assert ok, info
 
 
