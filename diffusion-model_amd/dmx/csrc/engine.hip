@@ -288,6 +288,8 @@ struct dmx_model {
   size_t ws_cap = 0;
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
+  hipGraphExec_t gexec_k = nullptr;  // the same step captured kGraphSteps times back to back
+  hipGraph_t graph_k = nullptr;
   dmx::GraphKey gkey{};
   bool has_graph = false;
   // debug taps: (name, device pointer into the workspace, element count, C)
@@ -1592,6 +1594,10 @@ static void drop_graph(dmx_model* m) {
   if (m->has_graph) {
     (void)hipGraphExecDestroy(m->gexec);
     (void)hipGraphDestroy(m->graph);
+    if (m->gexec_k) (void)hipGraphExecDestroy(m->gexec_k);
+    if (m->graph_k) (void)hipGraphDestroy(m->graph_k);
+    m->gexec_k = nullptr;
+    m->graph_k = nullptr;
     m->has_graph = false;
   }
 }
@@ -1626,11 +1632,7 @@ static void ensure_ws(dmx_model* m) {
     if (m->ws_mem) HIPCHK(hipFree(m->ws_mem));
     m->ws_mem = nullptr;
     m->ws_cap = 0;
-    if (m->has_graph) {
-      (void)hipGraphExecDestroy(m->gexec);
-      (void)hipGraphDestroy(m->graph);
-      m->has_graph = false;
-    }
+    drop_graph(m);
     HIPCHK(hipMalloc(&m->ws_mem, m->ws.off));
     m->ws_cap = m->ws.off;
   }
@@ -1946,10 +1948,7 @@ int dmx_model_create(dmx_ctx* ctx, int kind, int in_ch, int remove_deep_conv, dm
 int dmx_model_destroy(dmx_model* m) {
   return guarded([&] {
     if (!m) return;
-    if (m->has_graph) {
-      (void)hipGraphExecDestroy(m->gexec);
-      (void)hipGraphDestroy(m->graph);
-    }
+    drop_graph(m);
     for (void* p : m->owned) (void)hipFree(p);
     if (m->job_tables) (void)hipFree(m->job_tables);
     if (m->ws_mem) (void)hipFree(m->ws_mem);
@@ -2036,11 +2035,7 @@ int dmx_model_set_precision(dmx_model* m, int prec) {
   return guarded([&] {
     REQUIRE(m != nullptr, "null model");
     REQUIRE(prec >= 0 && prec <= 2, "precision must be 0 (fp32 MFMA), 1 (fp16x3 split) or 2 (fp16, config 4)");
-    if (m->prec != prec && m->has_graph) {
-      (void)hipGraphExecDestroy(m->gexec);
-      (void)hipGraphDestroy(m->graph);
-      m->has_graph = false;
-    }
+    if (m->prec != prec) drop_graph(m);
     m->prec = prec;
   });
 }
@@ -2120,6 +2115,8 @@ int dmx_step(dmx_model* m, const dmx_step_args* a, void* stream) {
   });
 }
 
+static constexpr int kGraphSteps = 8;
+
 int dmx_sample_loop(dmx_model* m, const dmx_step_args* a, int steps, int use_graph, void* stream) {
   return guarded([&] {
     REQUIRE(m != nullptr, "null model");
@@ -2144,11 +2141,7 @@ int dmx_sample_loop(dmx_model* m, const dmx_step_args* a, int steps, int use_gra
     std::memcpy(&key.a, a, sizeof(dmx_step_args));
     key.table_gen = m->ctx->table_gen;
     if (!(m->has_graph && key == m->gkey)) {
-      if (m->has_graph) {
-        (void)hipGraphExecDestroy(m->gexec);
-        (void)hipGraphDestroy(m->graph);
-        m->has_graph = false;
-      }
+      drop_graph(m);
       // plan + allocate outside capture, then capture the real launches
       m->ws.base = nullptr;
       m->ws.off = 0;
@@ -2177,8 +2170,30 @@ int dmx_sample_loop(dmx_model* m, const dmx_step_args* a, int steps, int use_gra
       HIPCHK(hipGraphInstantiate(&m->gexec, m->graph, nullptr, nullptr, 0));
       m->gkey = key;
       m->has_graph = true;
+      // kGraphSteps consecutive steps in one graph: the gap between two graph launches (≈9 µs of
+      // idle GPU per step in the replay trace, profiles/r03s2_trace_step.txt) is paid once per
+      // kGraphSteps steps.  t is decremented in-graph and the noise is keyed by (seed, t, sample), so
+      // the captured steps are the same launches as kGraphSteps replays of the one-step graph.
+      HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+      try {
+        for (int k = 0; k < kGraphSteps; ++k) {
+          m->ws.off = 0;
+          Run R{m, st, false, m->ws};
+          step_body(R, *a);
+          decrement_t_kernel<<<1, 64, 0, st>>>(tdev);
+        }
+      } catch (...) {
+        hipGraph_t g;
+        (void)hipStreamEndCapture(st, &g);
+        if (g) (void)hipGraphDestroy(g);
+        throw;
+      }
+      HIPCHK(hipStreamEndCapture(st, &m->graph_k));
+      HIPCHK(hipGraphInstantiate(&m->gexec_k, m->graph_k, nullptr, nullptr, 0));
     }
-    for (int i = 0; i < steps; ++i) HIPCHK(hipGraphLaunch(m->gexec, st));
+    int i = 0;
+    for (; i + kGraphSteps <= steps; i += kGraphSteps) HIPCHK(hipGraphLaunch(m->gexec_k, st));
+    for (; i < steps; ++i) HIPCHK(hipGraphLaunch(m->gexec, st));
   });
 }
 
