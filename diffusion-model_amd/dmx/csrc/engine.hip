@@ -1436,6 +1436,7 @@ struct FwdIn {
   const int64_t* t; int t_stride;
   const int64_t* y; int y_null_first; int64_t y_null;
   const float* vals; const float* mask; int cond_rows;
+  int64_t* t_next = nullptr;  // multi-step graphs: where the embedding kernel stores t - 1
 };
 
 // UnetCond trunk (models/unet_cond_geom.py:52-76): returns the (N,H,W,64) feature
@@ -1448,6 +1449,7 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
     std::memset(&e, 0, sizeof(e));
     e.t = in.t;
     e.t_stride = in.t_stride;
+    e.t_next = in.t_stride == 0 ? in.t_next : nullptr;
     e.t_mod = in.n_x < N ? in.n_x : 0;
     e.tmax = m->ctx->tmax;
     e.y = m->kind == DMX_UNET ? nullptr : in.y;
@@ -1658,11 +1660,13 @@ static void run_planned(dmx_model* m, hipStream_t st, F&& body) {
   if (m->ws.off != planned) throw Error(DMX_E_INTERNAL, "workspace plan / run mismatch");
 }
 
-static void step_body(Run& R, const dmx_step_args& a) {
+// t_next (multi-step sample-loop graphs): the step's t - 1 is stored there by the embedding kernel.
+static void step_body(Run& R, const dmx_step_args& a, int64_t* t_next = nullptr) {
   dmx_model* m = R.m;
   const bool cfg = m->kind != DMX_UNET && a.guidance > 0.f && a.y != nullptr;
   const int N = cfg ? 2 * a.n : a.n;
   FwdIn in{a.x_in, a.n, a.t, a.t_stride, a.y, cfg ? 1 : 0, a.null_label, a.vals, a.mask, a.n};
+  in.t_next = t_next;
   float* feat = unet_trunk(R, in, N, a.h, a.w);
   if (R.plan) return;
   StepTailParams p;
@@ -2171,16 +2175,21 @@ int dmx_sample_loop(dmx_model* m, const dmx_step_args* a, int steps, int use_gra
       m->gkey = key;
       m->has_graph = true;
       // kGraphSteps consecutive steps in one graph: the gap between two graph launches (≈9 µs of
-      // idle GPU per step in the replay trace, profiles/r03s2_trace_step.txt) is paid once per
-      // kGraphSteps steps.  t is decremented in-graph and the noise is keyed by (seed, t, sample), so
-      // the captured steps are the same launches as kGraphSteps replays of the one-step graph.
+      // idle GPU per step in the replay trace) is paid once per kGraphSteps steps.  Inside it, t
+      // alternates between the caller's scalar and a scratch scalar: step k reads one and its
+      // embedding kernel stores t - 1 in the other (no one-thread decrement launch per step; an even
+      // kGraphSteps ends in the caller's scalar).  The noise is keyed by (seed, t, sample), so the
+      // captured steps compute what kGraphSteps replays of the one-step graph compute.
+      static_assert(kGraphSteps % 2 == 0, "t ping-pong must end in the caller's buffer");
+      int64_t* tscr = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(m->range_flag) + 64);
       HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
       try {
         for (int k = 0; k < kGraphSteps; ++k) {
           m->ws.off = 0;
           Run R{m, st, false, m->ws};
-          step_body(R, *a);
-          decrement_t_kernel<<<1, 64, 0, st>>>(tdev);
+          dmx_step_args ak = *a;
+          ak.t = (k & 1) ? tscr : tdev;
+          step_body(R, ak, (k & 1) ? tdev : tscr);
         }
       } catch (...) {
         hipGraph_t g;

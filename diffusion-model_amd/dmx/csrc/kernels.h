@@ -38,6 +38,7 @@ struct EmbedParams {
   const float* wht; const float* bh;  // heads transposed: [256][Hsum]
   int hsum;
   float* out;                  // [n][hsum]
+  int64_t* t_next;             // sample-loop graphs (scalar t): block (0, 0) stores t - 1 here
 };
 
 // grid = (n, parts): every block recomputes the sample's 256-wide embedding (cheap) and
@@ -46,6 +47,8 @@ static __global__ __launch_bounds__(256) void embed_kernel(const EmbedParams p) 
   __shared__ float s[256], h[256], in24[24];
   const int n = blockIdx.x, k = threadIdx.x;
   int64_t t = p.t[(size_t)(p.t_mod ? n % p.t_mod : n) * p.t_stride];
+  // the next step's t in the other buffer of a multi-step graph (this step's readers keep p.t)
+  if (p.t_next != nullptr && n == 0 && blockIdx.y == 0 && k == 0) *p.t_next = t - 1;
   t = t < 1 ? 1 : (t > p.tmax ? p.tmax : t);
   float v = p.pos_table[(size_t)(t - 1) * 256 + k];
   if (p.y != nullptr) {
