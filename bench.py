@@ -220,7 +220,11 @@ def train_leg(args, dev, world=1, rank=0):
         y_used = torch.where(drop, torch.zeros_like(classes), classes)
         keep = (~drop).float().unsqueeze(1)
         eps, geom = model(z_noisy, t, y_used, cond_vals=vals * keep, cond_mask=mask * keep)
-        loss = F.mse_loss(eps, noise) + 0.5 * masked_geom_mse(geom, vals, mask * keep)
+        m_used = mask * keep
+        # world > 1: the geom term normalised by the GLOBAL mask mean, so the rank-averaged
+        # gradient is the global batch's (dmx.distributed.GradAllReducer)
+        denom = dd.global_mask_mean(m_used) if world > 1 else None
+        loss = F.mse_loss(eps, noise) + 0.5 * masked_geom_mse(geom, vals, m_used, denom=denom)
         opt.zero_grad(set_to_none=True)
         loss.backward()
         reducer.reduce()
@@ -613,10 +617,9 @@ def main():
     if rank == 0 or world == 1:
         model.load_state_dict(synth.unet_cond_geom_weights(0))
     model.to(dev).eval()
-    if world > 1:  # C1: broadcast the frozen weights once over RCCL (xGMI)
-        import torch.distributed as dist
-        for p in model.parameters():
-            dist.broadcast(p.data, src=0)
+    if world > 1:  # C1: broadcast the frozen weights once over RCCL (xGMI), one packed buffer
+        from dmx import distributed as dd
+        dd.broadcast_module(model)
     nm = model.native()
     d = diff.Diffuser(args.T, device=dev)
     tables = d.coef_tables(dev, True)

@@ -182,6 +182,8 @@ struct ConvW {
   _Float16* Bl = nullptr;
   _Float16* Fh = nullptr;       // the planes again in MFMA-fragment order (3x3 convs read by the
   _Float16* Fl = nullptr;       // halo kernel straight into registers; igemm_halo.h frag_planes_kernel)
+  _Float16* Uh = nullptr;       // 3x3 convs: Winograd F(2x2, 3x3) weights U = G g Gᵀ, split, fragment
+  _Float16* Ul = nullptr;       // order (igemm_wino.h wino_pack_kernel), same 2^e scale as Bh / Bl
   float inv_scale = 1.f;
   float* bias = nullptr;
   int cin = 0, cout = 0, taps = 0, kpad = 0, npad = 0, phases = 1;
@@ -296,6 +298,7 @@ struct dmx_model {
   bool debug = false;
   int prec = 1;  // 0: fp32 MFMA (exact fp32 products), 1: fp16 hi/lo x3 split MFMA, 2: fp16 (config 4)
   int* range_flag = nullptr;  // device int: an output went non-finite (kernels.h flag_nonfinite)
+  int64_t* t_scratch = nullptr;  // device int64: the 8-step graph's second t scalar (own allocation)
 
   std::vector<std::pair<std::string, std::pair<const float*, size_t>>> taps;
   // Weight packing replay (dmx_model_refresh): every device-side repack / copy of the caller's
@@ -345,6 +348,10 @@ static void split_planes(ConvW& c, hipStream_t st, unsigned* slot) {
     const size_t chunks = n / 8;
     frag_planes_kernel<<<(int)std::min<size_t>((chunks + 255) / 256, 8192), 256, 0, st>>>(c.Bh, c.Bl, c.Fh, c.Fl,
                                                                                           c.npad, c.kpad);
+    HIPCHK(hipGetLastError());
+  }
+  if (c.Uh != nullptr) {  // max|U| <= 2.25 max|w|: the scaled U stays below 2^15 (f16-normal hi and lo)
+    launch_wino_pack(c.B, c.kpad, c.cin, c.cout, scale, c.Uh, c.Ul, st);
     HIPCHK(hipGetLastError());
   }
 }
@@ -427,6 +434,17 @@ struct Packer {
       m->owned.push_back(l);
       c.Fh = static_cast<_Float16*>(h);
       c.Fl = static_cast<_Float16*>(l);
+      if (c.taps == 9 && c.cin % 16 == 0) {  // Winograd candidate (gemm(): wino_ok)
+        const size_t nu = (size_t)16 * c.cout * c.cin;
+        HIPCHK(hipMalloc(&h, nu * sizeof(_Float16)));
+        m->owned.push_back(h);
+        HIPCHK(hipMalloc(&l, nu * sizeof(_Float16)));
+        m->owned.push_back(l);
+        c.Uh = static_cast<_Float16*>(h);
+        c.Ul = static_cast<_Float16*>(l);
+        m->owned_bytes[static_cast<const char*>(h)] = nu * sizeof(_Float16);  // DMX_CHECK ranges
+        m->owned_bytes[static_cast<const char*>(l)] = nu * sizeof(_Float16);
+      }
     }
     split_planes(c, st, absmax_slot());
   }
@@ -653,6 +671,11 @@ static void finalize_model(dmx_model* m, hipStream_t st) {
     m->owned.push_back(f);
     m->range_flag = static_cast<int*>(f);
     HIPCHK(hipMemsetAsync(f, 0, 256, st));
+    void* t = nullptr;
+    HIPCHK(hipMalloc(&t, 256));
+    m->owned.push_back(t);
+    m->t_scratch = static_cast<int64_t*>(t);
+    HIPCHK(hipMemsetAsync(t, 0, 256, st));
   }
   HIPCHK(hipStreamSynchronize(st));
   // the registered tensors stay referenced only by dmx_model_refresh / training (include/dmx.h)
@@ -849,6 +872,23 @@ static int halo_ms_mode() {
 }
 static bool halo_ms_enabled() { return halo_ms_mode() != 0; }
 
+// DMX_WINO (same-box A/B): 1 (default) the halo convs at 16x16 / 32x32 run as Winograd F(2x2, 3x3)
+// (igemm_wino.h) in the x3 mode; 0 keeps the direct halo kernels.
+static bool wino_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("DMX_WINO");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return v;
+}
+// The Winograd conv replaces a halo conv (hbn > 0) with an fp32 source in the x3 (fp32-semantics)
+// mode: 64-tile x 64-channel blocks, 16-channel chunks.
+static bool wino_ok(const Run& R, int hbn, int src_C, int H, int W, const ConvW& cw, bool planes_src) {
+  return wino_enabled() && hbn > 0 && R.m->prec == 1 && !planes_src && cw.Uh != nullptr && (W == 16 || W == 32) &&
+         H % 2 == 0 && (H * W) % 256 == 0 && src_C % 16 == 0 && cw.cout % 64 == 0 &&
+         (size_t)16 * cw.cout * src_C * 2 < ((size_t)1 << 31);
+}
+
 // Low-resolution halo conv (igemm_halo.h, W = 8 / 4 square maps): 256-pixel tiles of whole samples,
 // K split over 32-channel chunks until the grid has >= 256 blocks.  Returns the output-channel tile
 // (0: not applicable) and the split count / chunks per split.
@@ -924,7 +964,8 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   }
   float* partial = splits > 1 ? R.ws.get<float>((size_t)splits * M * cw.cout) : nullptr;
   const int rgrp = (splits == 1 && (H * W) % 32 == 0) ? 32 : 1;
-  const int rrows = cw.phases * H * W / rgrp;
+  const bool wino = wino_ok(R, hbn, s.C, H, W, cw, ash != nullptr);
+  const int rrows = wino ? H * W / 16 : cw.phases * H * W / rgrp;  // GroupNorm partial rows per sample
   if (defer != nullptr) {
     defer->fused = splits > 1 && epi == EPI_STATS && !R.m->debug &&
                    H * W * (cw.cout / 4) <= RN_MAXV * 1024;  // (debug taps read the raw conv output)
@@ -989,6 +1030,8 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   xp.gn_cnt = 0;
   xp.gn_gamma = xp.gn_beta = nullptr;
   xp.gn_res = nullptr;
+  xp.Uh = xp.Ul = nullptr;
+  xp.u_bytes = 0;
   {
     const size_t a_el = (size_t)N * p.Hin * p.Win * s.C;
     const size_t ab = a_el * (ash != nullptr ? 2 : 4), bb = (size_t)cw.npad * cw.kpad * 2;
@@ -1057,6 +1100,19 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
       xp.gn_gamma = gn->gamma;
       xp.gn_beta = gn->beta;
       xp.gn_res = gn->res;
+    }
+    if (wino) {  // Winograd F(2x2, 3x3): 64 tiles (256 pixels) x 64 channels per block (igemm_wino.h)
+      xp.Uh = cw.Uh;
+      xp.Ul = cw.Ul;
+      xp.u_bytes = (unsigned)((size_t)16 * cw.cout * s.C * 2);
+      check_range(R, cw.Uh, xp.u_bytes, "U hi");
+      check_range(R, cw.Ul, xp.u_bytes, "U lo");
+      std::snprintf(nm, sizeof nm, "wino_kernel<%d, %d>", W, gna);
+      R.begin(nm, flops, bytes);
+      launch_wino(W, gna, xp, dim3(M / 256, cw.cout / 64, 1), R.st);
+      R.end();
+      HIPCHK(hipGetLastError());
+      return rrows;
     }
     std::snprintf(nm, sizeof nm, "igemm_halo_kernel<%d, %d, %d, %d, %d, %d>", hbn, (int)EPI_STATS, sa, x1 ? 1 : 0, W,
                   gna);
@@ -2172,8 +2228,7 @@ int dmx_sample_loop(dmx_model* m, const dmx_step_args* a, int steps, int use_gra
       }
       HIPCHK(hipStreamEndCapture(st, &m->graph));
       HIPCHK(hipGraphInstantiate(&m->gexec, m->graph, nullptr, nullptr, 0));
-      m->gkey = key;
-      m->has_graph = true;
+      m->has_graph = true;  // owns gexec / graph from here (drop_graph frees them on any failure below)
       // kGraphSteps consecutive steps in one graph: the gap between two graph launches (≈9 µs of
       // idle GPU per step in the replay trace) is paid once per kGraphSteps steps.  Inside it, t
       // alternates between the caller's scalar and a scratch scalar: step k reads one and its
@@ -2181,7 +2236,7 @@ int dmx_sample_loop(dmx_model* m, const dmx_step_args* a, int steps, int use_gra
       // kGraphSteps ends in the caller's scalar).  The noise is keyed by (seed, t, sample), so the
       // captured steps compute what kGraphSteps replays of the one-step graph compute.
       static_assert(kGraphSteps % 2 == 0, "t ping-pong must end in the caller's buffer");
-      int64_t* tscr = reinterpret_cast<int64_t*>(reinterpret_cast<char*>(m->range_flag) + 64);
+      int64_t* tscr = m->t_scratch;
       HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
       try {
         for (int k = 0; k < kGraphSteps; ++k) {
@@ -2195,10 +2250,16 @@ int dmx_sample_loop(dmx_model* m, const dmx_step_args* a, int steps, int use_gra
         hipGraph_t g;
         (void)hipStreamEndCapture(st, &g);
         if (g) (void)hipGraphDestroy(g);
+        drop_graph(m);
         throw;
       }
-      HIPCHK(hipStreamEndCapture(st, &m->graph_k));
-      HIPCHK(hipGraphInstantiate(&m->gexec_k, m->graph_k, nullptr, nullptr, 0));
+      const hipError_t ec = hipStreamEndCapture(st, &m->graph_k);
+      const hipError_t ei = ec == hipSuccess ? hipGraphInstantiate(&m->gexec_k, m->graph_k, nullptr, nullptr, 0) : ec;
+      if (ei != hipSuccess) {  // never leave a key that claims a graph pair without the 8-step exec
+        drop_graph(m);
+        HIPCHK(ei);
+      }
+      m->gkey = key;  // only once both graphs are instantiated
     }
     int i = 0;
     for (; i + kGraphSteps <= steps; i += kGraphSteps) HIPCHK(hipGraphLaunch(m->gexec_k, st));

@@ -1,0 +1,379 @@
+// dmx — split-precision 3x3 convolution as Winograd F(2x2, 3x3) on the f16 matrix cores, gfx950.
+//
+// Reference op: nn.Conv2d(k=3, padding=1, bias=False) of every ResBlock (models/unet_cond.py:17-23).
+//
+// A 3x3 / pad-1 convolution of a 2x2 output tile is Y = Aᵀ [ (G g Gᵀ) ⊙ (Bᵀ d B) ] A with d the 4x4
+// input patch of the tile (zero outside the image) and the 4x4 "positions" xi = (i, j):
+//   Bᵀ = [[1, 0,-1, 0], [0, 1, 1, 0], [0,-1, 1, 0], [0, 1, 0,-1]],  G = [[1,0,0], [½,½,½], [½,-½,½], [0,0,1]],
+//   Aᵀ = [[1, 1, 1, 0], [0, 1,-1,-1]].
+// Summed over input channels, each position is an independent GEMM
+//   M_xi[tile, cout] = sum_cin V_xi[tile, cin] * U_xi[cin, cout],   V = Bᵀ d B,  U = G g Gᵀ,
+// i.e. 16 multiply-adds per 4 output pixels instead of 36: 2.25x fewer MFMAs than the direct conv.
+// Precision is the direct kernels' (igemm_x3.h): V is formed in fp32 (sums / differences of input
+// values, one rounding each), U in double on the device at load time (wino_pack_kernel), both split
+// into f16 hi + lo and multiplied as al*bh + ah*bl + ah*bh with fp32 accumulation; the output
+// transform runs in fp32.  Every constant of B, G, A is ±1 or ½, so no transform step amplifies
+// rounding beyond the sums themselves (F(2x2,3x3) is the well-conditioned member of the family).
+//
+// Block: 512 threads = 8 waves, 64 tiles (256 output pixels = whole image rows of one sample at
+// W = 32 / one whole sample at W = 16) x 64 output channels, all 16 positions.  Wave w owns the two
+// positions (i, 2jp) and (i, 2jp + 1), i = w / 2, jp = w % 2: accumulators 2 positions x 2 (32-tile)
+// x 2 (32-channel) MFMA tiles = 128 VGPRs.  K walks 16-channel chunks (one k16 MFMA step):
+//   * the chunk's input halo ((rows + 2) x (W + 2) pixels x 16 channels, fp32, GroupNorm (+ residual)
+//     + GELU applied for GNA = 1 / 2 exactly as igemm_halo_kernel does) is staged once in LDS, with
+//     even and odd columns in separate planes so the 2-pixel tile stride becomes a 1-pixel stride
+//     (conflict-free ds_read_b128 with the row pitches below);
+//   * each wave forms ITS OWN A fragments V_(i,j)[tile, 8 channels] straight from the halo: two input
+//     rows (Bᵀ row i) x three input columns (B columns j) — 5 fma per channel for both positions,
+//     then the hi / lo split;
+//   * B (U) fragments come straight from the fragment-ordered planes into registers (1 KB coalesced
+//     per fragment, L2-resident), each reloaded for the next chunk right after its last MFMA;
+//   * one barrier per chunk (halo double buffer).
+// Epilogue: in four passes of (32 tiles x 32 channels) the 16 position accumulators go through LDS,
+// every thread applies Aᵀ M A to two tiles of one channel in a fixed order, stores the 2x2 pixels
+// (NHWC fp32) and the GroupNorm (sum, sum of squares) partials of 16-pixel x 32-channel groups
+// (HW / 16 partial rows per sample: the caller's consumers reduce a sample's partials in any layout).
+#pragma once
+#include "common.h"
+#include "igemm.h"
+#include "igemm_x3.h"
+#include "source.h"
+
+namespace dmx {
+
+// U = G g Gᵀ of one 3x3 kernel for position (i, j), in double (exact products of ½-multiples).
+DMX_DEV double wino_u(const double (&g)[3][3], int i, int j) {
+  double r[3];  // (G g)[i][b]
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    const double a0 = g[0][b], a1 = g[1][b], a2 = g[2][b];
+    r[b] = i == 0 ? a0 : i == 1 ? 0.5 * (a0 + a1 + a2) : i == 2 ? 0.5 * (a0 - a1 + a2) : a2;
+  }
+  return j == 0 ? r[0] : j == 1 ? 0.5 * (r[0] + r[1] + r[2]) : j == 2 ? 0.5 * (r[0] - r[1] + r[2]) : r[2];
+}
+
+// Weight transform + split into MFMA-fragment order: B operand of v_mfma_f32_32x32x16_f16 for
+// position xi, output channels 32 nb .. +31, input channels 16 kk .. +15 is 64 lanes x 8 f16 (lane
+// (fr, fh): channel 32 nb + fr, inputs 16 kk + 8 fh .. +7), stored 1 KB contiguous at
+// ((xi * NB + nb) * KK + kk) * 512 halves.  B: packed fp32 [npad][kpad] (k = tap * cin + c).
+static __global__ void wino_pack_kernel(const float* B, int kpad, int cin, int cout, float scale, _Float16* uh,
+                                        _Float16* ul) {
+  const int NB = cout / 32, KK = cin / 16;
+  const size_t total = (size_t)16 * NB * KK * 64;
+  for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (size_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(q & 63);
+    const size_t f = q >> 6;
+    const int kk = (int)(f % KK), nb = (int)((f / KK) % NB), xi = (int)(f / ((size_t)KK * NB));
+    const int co = 32 * nb + (lane & 31), c0 = 16 * kk + 8 * (lane >> 5);
+    half8 h, l;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      double g[3][3];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) g[t / 3][t % 3] = (double)B[(size_t)co * kpad + (size_t)t * cin + c0 + e];
+      const float u = (float)(wino_u(g, xi >> 2, xi & 3) * (double)scale);
+      const _Float16 hh = (_Float16)u;
+      h[e] = hh;
+      l[e] = (_Float16)(u - (float)hh);
+    }
+    *reinterpret_cast<half8*>(uh + q * 8) = h;
+    *reinterpret_cast<half8*>(ul + q * 8) = l;
+  }
+}
+
+template <int W, int GNA>
+__global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
+  static_assert(W == 32 || W == 16, "Winograd conv: image width 16 or 32");
+  const IgemmParams& p = P.g;
+  constexpr int TW = W / 2;                 // tiles per tile row
+  constexpr int TR = 256 / W;               // output rows of the block (64 tiles)
+  constexpr int HR = TR + 2, HC = W + 2;    // halo rows / columns
+  constexpr int RP = W == 32 ? 88 : 46;     // parity-plane row pitch in 16-byte units (see header)
+  constexpr int HBUF = HR * 2 * RP * 4;     // floats per halo buffer
+  constexpr int CK = 16;                    // channels per chunk
+  constexpr int NPC = HR * HC * (CK / 4);   // float4 pieces per chunk
+  constexpr int NPI = (NPC + 511) / 512;    // pieces per thread
+  constexpr int EPP = 36;                   // epilogue LDS row pitch (32 tiles + 4)
+  constexpr int EPF = 16 * 32 * EPP;        // epilogue floats (one 32 x 32 pass, 16 positions)
+  constexpr int LDSF = 2 * HBUF + 1024 > EPF ? 2 * HBUF + 1024 : EPF;
+  __shared__ __attribute__((aligned(16))) float lds[LDSF];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wi = wid >> 1, jp = wid & 1;
+  int mt, nt, bz;
+  xcd_tile(mt, nt, bz);
+  const int m0 = mt * 256;
+  const int HW = p.H * W, C = p.src.C;
+  const int nsmp = m0 / HW, y0 = (m0 - nsmp * HW) / W;
+  const int nch = C / CK;
+
+  // ---- halo pieces of this thread: (halo pixel, 4-channel quad), global element offset (chunk 0)
+  // or -1 (zero padding), LDS float offset
+  int hoff[NPI], hls[NPI];
+#pragma unroll
+  for (int k = 0; k < NPI; ++k) {
+    const int e = tid + 512 * k;
+    const int h = e >> 2, q = e & 3;
+    const int hy = h / HC, hx = h - hy * HC;
+    const int y = y0 + hy - 1, x = hx - 1;
+    const bool ok = e < NPC && y >= 0 && y < p.H && x >= 0 && x < W;
+    hoff[k] = ok ? (((nsmp * p.H + y) * W + x) * C + q * 4) : -1;
+    // pieces past the halo store to a scratch slot of their own (no divergent branch around the store)
+    hls[k] = e < NPC ? ((hy * 2 + (hx & 1)) * RP * 4 + (hx >> 1) * 20 + q * 4) : 2 * HBUF + (tid & 255) * 4;
+  }
+  const __amdgpu_buffer_rsrc_t rA = rsrc_of(p.src.src0, P.a_bytes);
+  const __amdgpu_buffer_rsrc_t rRes = rsrc_of(GNA == 2 ? (const void*)P.gn_res : (const void*)p.src.src0, P.a_bytes);
+
+  // ---- GroupNorm(1, C) statistics of sample nsmp (as igemm_halo_kernel / norm_kernel reduce them)
+  float2 gst = make_float2(0.f, 0.f);
+  if constexpr (GNA) {
+    __shared__ double gr1[4], gr2[4];
+    __shared__ float2 gst_s;
+    if (tid < 256) {
+      const float2* rp = P.gn_rowpart + (size_t)nsmp * P.gn_cnt;
+      double s1 = 0.0, s2 = 0.0;
+      for (int i = tid; i < P.gn_cnt; i += 256) {
+        const float2 q = rp[i];
+        s1 += (double)q.x;
+        s2 += (double)q.y;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        s1 += __shfl_xor(s1, o, 64);
+        s2 += __shfl_xor(s2, o, 64);
+      }
+      if ((tid & 63) == 0) {
+        gr1[tid >> 6] = s1;
+        gr2[tid >> 6] = s2;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const double cntd = (double)HW * (double)C;
+      const double mean = ((gr1[0] + gr1[1]) + (gr1[2] + gr1[3])) / cntd;
+      double var = ((gr2[0] + gr2[1]) + (gr2[2] + gr2[3])) / cntd - mean * mean;
+      var = var < 0.0 ? 0.0 : var;
+      gst_s = make_float2((float)mean, (float)(1.0 / sqrt(var + 1e-5)));
+    }
+    __syncthreads();
+    gst = gst_s;
+  }
+
+  floatx4 ha[NPI];
+  floatx4 hr[GNA == 2 ? NPI : 1];
+  floatx4 ggam = {0.f, 0.f, 0.f, 0.f}, gbet = {0.f, 0.f, 0.f, 0.f};
+  auto load_halo = [&](int c) {
+    if constexpr (GNA) {  // every piece of this thread holds the same channel quad (512 % 4 == 0)
+      const int ch = c * CK + (tid & 3) * 4;
+      ggam = ld4(P.gn_gamma + ch);
+      gbet = ld4(P.gn_beta + ch);
+    }
+#pragma unroll
+    for (int k = 0; k < NPI; ++k) {
+      const int off = hoff[k] >= 0 ? (hoff[k] + c * CK) * 4 : kOOB;
+      ha[k] = bload_f4(rA, off, 0);
+      if constexpr (GNA == 2) hr[k] = bload_f4(rRes, off, 0);
+    }
+  };
+  auto store_halo = [&](int buf) {
+    float* hb = lds + buf * HBUF;
+#pragma unroll
+    for (int k = 0; k < NPI; ++k) {
+      floatx4 v = ha[k];
+      if constexpr (GNA) {  // GroupNorm (+ residual) + GELU of the raw source; zero padding stays zero
+        v = gn_apply4v(v, gst, ggam, gbet, GNA == 1 ? 1 : 0);
+        if constexpr (GNA == 2) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = gelu(hr[k][j] + v[j]);
+        }
+        if (hoff[k] < 0) v = floatx4{0.f, 0.f, 0.f, 0.f};
+      }
+      *reinterpret_cast<floatx4*>(hb + hls[k]) = v;
+    }
+  };
+
+  // ---- U fragments: positions xi0, xi0 + 1 (wave-uniform), column tiles 2 nt, 2 nt + 1
+  const int xi0 = 4 * wi + 2 * jp;
+  const int NB = p.Cout / 32, KK = C / 16;
+  const __amdgpu_buffer_rsrc_t rUh = rsrc_of(P.Uh, P.u_bytes), rUl = rsrc_of(P.Ul, P.u_bytes);
+  int ub[2][2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) ub[q][n] = (((xi0 + q) * NB + 2 * nt + n) * KK) * 1024;
+  const int voff = lane * 16;
+  half8 bh[2][2], bl[2][2];
+  int cnext = 0;  // chunk whose fragments load_b(.., -1) fetches
+  auto load_b = [&](int q, int n, int c) {
+    const int cc = c < 0 ? cnext : c;
+    bh[q][n] = bload_h8(rUh, voff, ub[q][n] + cc * 1024);
+    bl[q][n] = bload_h8(rUl, voff, ub[q][n] + cc * 1024);
+  };
+
+  // ---- A fragments: rows (Bᵀ row wi) and columns (B columns of positions 2jp, 2jp + 1)
+  // T(col) = d(ra, col) + sr d(rb, col);  V_a = T(cp) - T(cq);  V_b = T(cq) + sb T(cs)
+  const int ra = wi == 0 ? 0 : wi == 2 ? 2 : 1;
+  const int rb = wi == 0 ? 2 : wi == 2 ? 1 : wi == 1 ? 2 : 3;
+  const float sr = wi == 1 ? 1.f : -1.f;
+  const int cp = jp ? 2 : 0, cq = jp ? 1 : 2, cs = jp ? 3 : 1;
+  const float sb = jp ? -1.f : 1.f;
+  auto coff = [&](int col) { return (col & 1) * RP * 4 + (col >> 1) * 20; };
+  const int oa = ra * 8 * RP, ob = rb * 8 * RP;
+  const int op = coff(cp), oq = coff(cq), os = coff(cs);
+  const int fr = lane & 31, fh = lane >> 5;
+  int tb[2];
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb) {
+    const int t = 32 * mb + fr, ty = t / TW, tx = t - ty * TW;
+    tb[mb] = ty * 16 * RP + tx * 20 + 8 * fh;
+  }
+  half8 ah[2], al[2];  // [position] of the current m tile
+  auto build = [&](int buf, int mb) {
+    const float* hb = lds + buf * HBUF;
+    {
+      floatx4 T[3][2];
+      const int oc[3] = {op, oq, os};
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float* pa = hb + tb[mb] + oa + oc[k];
+        const float* pb = hb + tb[mb] + ob + oc[k];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const floatx4 da = *reinterpret_cast<const floatx4*>(pa + 4 * h);
+          const floatx4 db = *reinterpret_cast<const floatx4*>(pb + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) T[k][h][e] = fmaf(db[e], sr, da[e]);
+        }
+      }
+      unsigned vh[2][4], vl[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const float a0 = T[0][h][e] - T[1][h][e], a1 = T[0][h][e + 1] - T[1][h][e + 1];
+          const float b0 = fmaf(T[2][h][e], sb, T[1][h][e]), b1 = fmaf(T[2][h][e + 1], sb, T[1][h][e + 1]);
+          split2u(a0, a1, vh[0][2 * h + e / 2], vl[0][2 * h + e / 2]);
+          split2u(b0, b1, vh[1][2 * h + e / 2], vl[1][2 * h + e / 2]);
+        }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        ah[q] = __builtin_bit_cast(half8, (u32x4){vh[q][0], vh[q][1], vh[q][2], vh[q][3]});
+        al[q] = __builtin_bit_cast(half8, (u32x4){vl[q][0], vl[q][1], vl[q][2], vl[q][3]});
+      }
+    }
+  };
+
+  floatx16 acc[2][2][2];  // [position][m tile][n tile]
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[q][i][j][r] = 0.f;
+
+  // ---- prologue: chunk 0's halo in LDS, its U fragments and chunk 1's halo in flight
+  load_halo(0);
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) load_b(q, n, 0);
+  store_halo(0);
+  load_halo(min(1, nch - 1));
+  __syncthreads();
+
+  // Per chunk: next halo to LDS (its registers free before the A build), m tile 0's A fragments and
+  // MFMAs, m tile 1's, with chunk c + 2's halo loads issued between the two; every U fragment is
+  // reloaded for chunk c + 1 right after its last MFMA of chunk c.  Register peak: 128 accumulators +
+  // 32 U + one m tile's A fragments + the build temporaries / the halo pieces in flight.
+  auto mfmas = [&](int i, bool last) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[q], bh[q][n], acc[q][i][n], 0, 0, 0);
+        acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[q], bl[q][n], acc[q][i][n], 0, 0, 0);
+        acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[q], bh[q][n], acc[q][i][n], 0, 0, 0);
+        if (last) load_b(q, n, -1);  // (always: a static load sequence keeps the vmcnt waits exact)
+      }
+  };
+  // Every global load is issued unconditionally (chunk indices clamped to the last chunk; the extra
+  // loads of the final iterations are never used) so the vector-memory counter sequence is the same
+  // on every iteration and each wait covers exactly the loads it needs.
+  for (int c = 0; c < nch; ++c) {
+    store_halo((c + 1) & 1);  // buffer (c + 1) & 1 was last read by chunk c - 1 (c + 1 = nch: unused)
+    build(c & 1, 0);
+    mfmas(0, false);
+    build(c & 1, 1);
+    load_halo(min(c + 2, nch - 1));
+    cnext = min(c + 1, nch - 1);
+    mfmas(1, true);
+    __syncthreads();
+  }
+
+  // ---- epilogue: Aᵀ M A per tile, four passes of 32 tiles x 32 channels through LDS
+  const int HW16 = HW / 16, nseg = p.Cout / 32;
+  const int tile0 = (m0 - nsmp * HW) / 4;  // first tile of the block inside its sample
+  const int cc = tid & 31, tp = tid >> 5;  // output task: channel cc, tiles 2 tp, 2 tp + 1
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int n = 0; n < 2; ++n) {
+      // positions -> LDS [xi][channel][tile] (rows of a lane's accumulator are 4 consecutive tiles)
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          floatx4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[q][mb][n][4 * k + e] * P.inv_scale;
+          *reinterpret_cast<floatx4*>(&lds[((xi0 + q) * 32 + fr) * EPP + 8 * k + 4 * fh]) = v;
+        }
+      __syncthreads();
+      float m[16][2];
+#pragma unroll
+      for (int xi = 0; xi < 16; ++xi) {
+        const f32x2 v = *reinterpret_cast<const f32x2*>(&lds[(xi * 32 + cc) * EPP + 2 * tp]);
+        m[xi][0] = v.x;
+        m[xi][1] = v.y;
+      }
+      const int col = 64 * nt + 32 * n + cc;
+      const float bias = p.bias != nullptr ? p.bias[col] : 0.f;
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        float z[4][2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          z[i][0] = (m[4 * i][e] + m[4 * i + 1][e]) + m[4 * i + 2][e];
+          z[i][1] = (m[4 * i + 1][e] - m[4 * i + 2][e]) - m[4 * i + 3][e];
+        }
+        const int t = 32 * mb + 2 * tp + e, ty = t / TW, tx = t - ty * TW;
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const float y = (r == 0 ? (z[0][s] + z[1][s]) + z[2][s] : (z[1][s] - z[2][s]) - z[3][s]) + bias;
+            const int oy = y0 + 2 * ty + r, ox = 2 * tx + s;
+            p.out[(((size_t)nsmp * p.H + oy) * W + ox) * p.Cout + col] = y;
+            s1 += y;
+            s2 += y * y;
+          }
+      }
+      // partial of 4 tiles (16 pixels) x 32 channels = this wave's 64 lanes
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        s1 += __shfl_xor(s1, o, 64);
+        s2 += __shfl_xor(s2, o, 64);
+      }
+      if (lane == 0) {
+        const int g = (tile0 + 32 * mb + 4 * wid) / 4;
+        p.rowpart[((size_t)nsmp * HW16 + g) * nseg + 2 * nt + n] = make_float2(s1, s2);
+      }
+      __syncthreads();
+    }
+}
+
+}  // namespace dmx

@@ -46,6 +46,10 @@ struct X3Params {
   const float* gn_gamma;
   const float* gn_beta;
   const float* gn_res;       // GNA = 2: GELU(res + GroupNorm(src)) (a residual ResBlock's output)
+  // Winograd F(2x2, 3x3) weights (igemm_wino.h): U = G g Gᵀ split hi / lo, fragment order
+  const _Float16* Uh;
+  const _Float16* Ul;
+  unsigned u_bytes;          // bytes of one U plane (16 * Cout * Cin f16)
 };
 
 

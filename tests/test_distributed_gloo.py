@@ -85,6 +85,27 @@ def _bcast_gather(rank, world):
     return float(m.weight.sum()), float(m.bias.sum()), None if full is None else full.flatten().tolist()
 
 
+def _bcast_packed(rank, world):
+    """C1 packed: a module with mixed dtypes goes out as one flattened buffer per dtype."""
+    m = torch.nn.Sequential(torch.nn.Linear(4, 3), torch.nn.Linear(3, 2))
+    m.register_buffer("steps", torch.zeros(2, dtype=torch.long))
+    if rank == 0:
+        with torch.no_grad():
+            for i, p in enumerate(m.parameters()):
+                p.copy_(torch.arange(p.numel(), dtype=p.dtype).reshape(p.shape) * (i + 1))
+            m.steps.fill_(7)
+    ts = [t.data for t in list(m.parameters()) + list(m.buffers())]
+    n = dd.broadcast_tensors(ts)
+    return n, [t.flatten().tolist() for t in ts]
+
+
+def test_broadcast_is_one_packed_message_per_dtype_world2():
+    res = run(_bcast_packed)
+    assert res[0][0] == res[1][0] == 2  # float32 parameters + the int64 buffer
+    assert res[0][1] == res[1][1]
+    assert res[1][1][-1] == [7.0, 7.0] or res[1][1][-1] == [7, 7]
+
+
 def test_broadcast_and_gather_world2():
     res = run(_bcast_gather)
     for r in (0, 1):

@@ -160,8 +160,9 @@ def unet_sd_overflow():
 def _train_job(rank, world, B=4):
     """train_latent_cond.py's loss on this rank's half of a B = 4 batch (28x28x4 latents),
     loss.backward() through dmx_train_backward, then GradAllReducer (gloo here, RCCL in bench).
-    geom mask all ones: the masked geom mean is then a plain mean, so the average of the two
-    half-batch gradients is exactly the full-batch gradient (up to fp32 summation order)."""
+    The geom mask is NOT uniform (the two halves have different mask sums): the geom term is
+    normalised by ``global_mask_mean`` (one scalar all-reduce), so the average of the two
+    half-batch gradients is the full-batch gradient (up to fp32 summation order)."""
     import torch.nn.functional as F
     from dmx import distributed as dd
     from dmx import synth
@@ -178,11 +179,13 @@ def _train_job(rank, world, B=4):
     y = torch.randint(1, 4, (B,), generator=g)
     vals = torch.rand((B, 12), generator=g)
     noise = torch.randn((B, 4, 28, 28), generator=g)
-    mask = torch.ones((B, 12))
+    mask = (torch.rand((B, 12), generator=g) > 0.4).float()
+    mask[:B // 2, :4] = 0.0  # rank 0's half holds fewer mask entries than rank 1's
     s, e = dd.shard_range(B, world, rank)
     sl = [a[s:e].to(dev) for a in (z, t, y, vals, mask, noise)]
     eps, geom = m(sl[0], sl[1], sl[2], cond_vals=sl[3], cond_mask=sl[4])
-    loss = F.mse_loss(eps, sl[5]) + 0.5 * masked_geom_mse(geom, sl[3], sl[4])
+    denom = dd.global_mask_mean(sl[4]) if world > 1 else None
+    loss = F.mse_loss(eps, sl[5]) + 0.5 * masked_geom_mse(geom, sl[3], sl[4], denom=denom)
     loss.backward()
     dd.GradAllReducer(m.parameters()).reduce()
     return {n: p.grad.detach().cpu() for n, p in m.named_parameters() if p.grad is not None}

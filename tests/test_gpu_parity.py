@@ -84,6 +84,25 @@ def test_unet_forward_vs_oracle_no_cond(model, cuda, unet_sd):
     assert rel(eps, e2) < TOL and rel(geom, g2) < TOL
 
 
+def test_unet_forward_bench_batch_vs_oracle(model, cuda, unet_sd, prec):
+    """One forward of 128 samples (the CFG batch of B=64): the batch at which the 16x16 / 32x32 convs
+    take their large-grid kernels — in x3 mode the Winograd F(2x2, 3x3) convs (igemm_wino.h) — checked
+    on eps itself (a CFG step's latent hides eps errors behind its (1-a)/sqrt(1-ab) factor)."""
+    g = torch.Generator().manual_seed(128)
+    N = 128
+    x = torch.randn((N, 4, 32, 32), generator=g)
+    t = torch.randint(1, 1001, (N,), generator=g)
+    y = torch.randint(0, 4, (N,), generator=g)
+    vals = torch.rand((N, 12), generator=g)
+    mask = (torch.rand((N, 12), generator=g) > 0.5).float()
+    with torch.no_grad():
+        eps, geom = model(x.to(cuda), t.to(cuda), y.to(cuda), cond_vals=vals.to(cuda), cond_mask=mask.to(cuda))
+        e2, g2 = ref.unet_cond_geom_forward(unet_sd, x, t, y, vals, mask)
+    ee, eg = rel(eps, e2), rel(geom, g2)
+    print(f"[forward N=128 {prec}] eps rel-L2 {ee:.2e}, geom {eg:.2e}")
+    assert ee < TOL and eg < TOL
+
+
 def test_uncond_unet_golden(golden, cuda):
     from dmx import synth
     from models.unet import Unet
