@@ -881,12 +881,44 @@ static bool wino_enabled() {
   }();
   return v;
 }
-// The Winograd conv replaces a halo conv (hbn > 0) with an fp32 source in the x3 (fp32-semantics)
-// mode: 64-tile x 64-channel blocks, 16-channel chunks.
-static bool wino_ok(const Run& R, int hbn, int src_C, int H, int W, const ConvW& cw, bool planes_src) {
-  return wino_enabled() && hbn > 0 && R.m->prec == 1 && !planes_src && cw.Uh != nullptr && (W == 16 || W == 32) &&
-         H % 2 == 0 && (H * W) % 256 == 0 && src_C % 16 == 0 && cw.cout % 64 == 0 &&
-         (size_t)16 * cw.cout * src_C * 2 < ((size_t)1 << 31);
+// The Winograd conv (x3 fp32-semantics mode, fp32 source, 64-tile x 64-channel blocks, 16-channel
+// chunks) replaces a halo conv (hbn > 0: 16 x 16 / 32 x 32) or, on 8 x 8 maps, the low-resolution
+// halo conv where 4-sample blocks fill >= 256 blocks without split-K (up1.0: 512 -> 512).
+// DMX_WINO_SPLIT (same-box A/B): 1 (default) Winograd also for the convs whose 64 x 64 blocks do
+// not fill 256 CUs, with K split over 16-channel chunks (slabs reduced like the other split convs).
+static bool wino_split_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("DMX_WINO_SPLIT");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return v;
+}
+// Winograd plan of a 3x3 conv given an fp32 source: 0 = not applicable, else the K split count
+// (1 = whole K) and *cps = 16-channel chunks per split.  Blocks: 64 tiles (8 rows of a 32-wide map,
+// one 16 x 16 sample, four 8 x 8 samples) x 64 output channels; decisions from Md (a batch and its
+// shards of the same per-rank size take the same ones).
+static int wino_plan(const Run& R, int src_C, int N, int H, int W, const ConvW& cw, int* cps) {
+  // (U-Net only: the VAE decoder keeps its per-sample-tiled direct convs, Run::tile_n)
+  if (!wino_enabled() || R.m->prec != 1 || R.m->kind == DMX_VAE || R.tile_n > 0 || cw.Uh == nullptr ||
+      cw.phases != 1 || cw.taps != 9)
+    return 0;
+  if (!((W == 32 && H % 8 == 0) || (W == 16 && H == 16) || (W == 8 && H == 8))) return 0;
+  const int Md = (R.tile_n > 0 ? R.tile_n : N) * H * W;
+  if (Md % 256 != 0 || src_C % 16 != 0 || cw.cout % 64 != 0 || (size_t)16 * cw.cout * src_C * 2 >= ((size_t)1 << 31))
+    return 0;
+  const int blocks = (Md / 256) * (cw.cout / 64), nch = src_C / 16;
+  int sp = 1, cp = nch;
+  if (blocks < 256) {
+    if (!wino_split_enabled()) return 0;
+    sp = std::max(1, std::min(nch, cdiv(256, blocks)));
+    cp = cdiv(nch, sp);
+    sp = cdiv(nch, cp);
+  }
+  if (cps != nullptr) *cps = cp;
+  return sp;
+}
+static bool wino_any(const Run& R, int src_C, int N, int H, int W, const ConvW& cw) {
+  return wino_plan(R, src_C, N, H, W, cw, nullptr) > 0;
 }
 
 // Low-resolution halo conv (igemm_halo.h, W = 8 / 4 square maps): 256-pixel tiles of whole samples,
@@ -933,6 +965,29 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   const int M = N * H * W;
   const int Md = (R.tile_n > 0 ? R.tile_n : N) * H * W;  // rows the decisions below are taken for
   if (cw.cout % 32 != 0) throw Error(DMX_E_INTERNAL, "gemm: Cout must be a multiple of 32");
+  if (src_mode == SRC_NCHW && epi == EPI_STATS && cw.taps == 9 && cw.phases == 1 && cw.cin == 4 && cw.cout == 64 &&
+      W % 32 == 0 && seg == 32 && cw.bias == nullptr && R.m->kind != DMX_VAE && gn == nullptr) {
+    // inc's first conv: direct fp32 conv of the NCHW input (kernels.h conv_in_kernel)
+    if (defer != nullptr) *defer = Deferred{};  // whole K, no slabs
+    if (R.plan) return H * W / 32;
+    ConvInParams q;
+    q.x = s.src0;
+    q.creal = s.C0 ? s.C0 : s.C;
+    q.n_mod = s.n_mod;
+    q.scale = s.scale;
+    q.B = cw.B;
+    q.cin = cw.cin;
+    q.kpad = cw.kpad;
+    q.out = out;
+    q.rowpart = rowpart;
+    q.H = H;
+    q.W = W;
+    R.begin("conv_in_kernel", 2.0 * M * 64.0 * 9.0 * q.creal, 4.0 * ((double)M * 64 + (double)M * q.creal));
+    conv_in_kernel<<<M / 32, 256, 0, R.st>>>(q);
+    R.end();
+    HIPCHK(hipGetLastError());
+    return H * W / 32;
+  }
   const int bn = (cw.cout % 128 == 0) ? 128 : 64;
   const int tiles128 = cdiv(Md, 128) * cdiv(cw.cout, bn) * cw.phases;
   const int bm = tiles128 >= 256 ? 128 : 64;  // 128-row tiles (split K if the grid is then small) from 256 tiles
@@ -945,27 +1000,32 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   // halo-staged 3x3 conv (igemm_halo.h): 256-pixel tiles of whole image rows (W = 16 / 32), the
   // chunk's input halo staged once for all nine taps; where it fills >= 256 blocks without split-K
   const int hbn = halo_bn(R, s.C, N, H, W, cw, epi, ash != nullptr || src_mode == SRC_PLAIN);
-  if (gn != nullptr && (hbn == 0 || ash != nullptr || src_mode != SRC_PLAIN))
-    throw Error(DMX_E_INTERNAL, "gemm: GroupNorm-on-load needs the halo conv on a plain fp32 source");
+  int wsp = 0, wcps = 0;
+  if (epi == EPI_STATS && src_mode == SRC_PLAIN && ash == nullptr) wsp = wino_plan(R, s.C, N, H, W, cw, &wcps);
+  const bool wino = wsp > 0;
+  if (gn != nullptr && ((hbn == 0 && !wino) || ash != nullptr || src_mode != SRC_PLAIN))
+    throw Error(DMX_E_INTERNAL, "gemm: GroupNorm-on-load needs the halo / Winograd conv on a plain fp32 source");
   int ms_splits = 1, ms_cps = 0;
-  const int msbn = hbn ? 0
+  const int msbn = (hbn || wino) ? 0
                        : halo_ms_bn(R, s.C, N, H, W, cw, epi, ash != nullptr || src_mode == SRC_PLAIN, &ms_splits,
                                     &ms_cps);
   const int bk = pp ? 32 : x3 ? 64 : IG_BK;
   const int nkt = cw.kpad / bk;
   int splits = 1, ksplit = nkt;
-  if (msbn) {  // low-resolution halo conv: K split over channel chunks (ksplit = chunks per split)
+  if (wino) {  // Winograd: K split over 16-channel chunks where 64 x 64 blocks do not fill the chip
+    splits = wsp;
+    ksplit = wcps;
+  } else if (msbn) {  // low-resolution halo conv: K split over channel chunks (ksplit = chunks per split)
     splits = ms_splits;
     ksplit = ms_cps;
-  } else if (!hbn && !pp && cw.phases == 1 && blocks < split_below() && nkt * bk >= 512) {  // split K below 2 blocks / CU
+  } else if (!hbn && !wino && !pp && cw.phases == 1 && blocks < split_below() && nkt * bk >= 512) {  // split K below 2 blocks / CU
     splits = std::min(std::min(8, std::max(2, 512 / blocks)), nkt * bk / 256);
     ksplit = cdiv(nkt, splits);
     splits = cdiv(nkt, ksplit);
   }
   float* partial = splits > 1 ? R.ws.get<float>((size_t)splits * M * cw.cout) : nullptr;
   const int rgrp = (splits == 1 && (H * W) % 32 == 0) ? 32 : 1;
-  const bool wino = wino_ok(R, hbn, s.C, H, W, cw, ash != nullptr);
-  const int rrows = wino ? H * W / 16 : cw.phases * H * W / rgrp;  // GroupNorm partial rows per sample
+  const int rrows = (wino && splits == 1) ? H * W / 16 : cw.phases * H * W / rgrp;  // GroupNorm partial rows / sample
   if (defer != nullptr) {
     defer->fused = splits > 1 && epi == EPI_STATS && !R.m->debug &&
                    H * W * (cw.cout / 4) <= RN_MAXV * 1024;  // (debug taps read the raw conv output)
@@ -1091,8 +1151,8 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
     HIPCHK(hipGetLastError());
     return rrows;
   }
-  if (hbn) {  // halo-staged 3x3 conv, 256-pixel x hbn tiles (igemm_halo.h)
-    dim3 gh(M / 256, cw.cout / hbn, 1);
+  if (hbn || wino) {  // halo-staged 3x3 conv, 256-pixel x hbn tiles (igemm_halo.h) / Winograd
+    dim3 gh(M / 256, hbn ? cw.cout / hbn : 1, 1);
     const int gna = gn != nullptr ? (gn->res != nullptr ? 2 : 1) : 0;
     if (gna) {
       xp.gn_rowpart = gn->rowpart;
@@ -1107,9 +1167,16 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
       xp.u_bytes = (unsigned)((size_t)16 * cw.cout * s.C * 2);
       check_range(R, cw.Uh, xp.u_bytes, "U hi");
       check_range(R, cw.Ul, xp.u_bytes, "U lo");
-      std::snprintf(nm, sizeof nm, "wino_kernel<%d, %d>", W, gna);
-      R.begin(nm, flops, bytes);
-      launch_wino(W, gna, xp, dim3(M / 256, cw.cout / 64, 1), R.st);
+      const int e = splits > 1 ? (int)EPI_PARTIAL : (int)EPI_STATS;
+      std::snprintf(nm, sizeof nm, "wino_kernel<%d, %d, %d>", W, gna, e);
+      R.begin(nm, flops, bytes + (splits > 1 ? 4.0 * splits * M * cw.cout : 0.0));
+      launch_wino(e, W, gna, xp, dim3(M / 256, cw.cout / 64, splits), R.st);
+      R.end();
+      HIPCHK(hipGetLastError());
+      if (splits == 1 || (defer != nullptr && defer->fused)) return rrows;
+      SplitkParams q{partial, splits, M, cw.cout, cw.bias, res, out, rowpart, seg, epi, R.m->prec == 0 ? 1 : 0};
+      R.begin("splitk_reduce_kernel", 0.0, 4.0 * (double)(splits + 1) * M * cw.cout);
+      splitk_reduce_kernel<<<cdiv(M * (cw.cout / 4), 256), 256, 0, R.st>>>(q);
       R.end();
       HIPCHK(hipGetLastError());
       return rrows;
@@ -1253,7 +1320,9 @@ static float* resblock(Run& R, const ResW& w, const SrcDesc& in, int mode, int N
   const int seg = 32;
   float* r1 = R.ws.get<float>((size_t)M * w.mid);
   float2* rp1 = R.ws.get<float2>((size_t)M * (w.mid / seg));
-  const bool planes = R.m->prec >= 1 && split_a_enabled() && w.c2.Bh != nullptr && w.mid >= 64;
+  // conv2 on the Winograd kernel reads the fp32 mid activation (GroupNorm-on-load or materialised)
+  const bool c2_wino = wino_any(R, w.mid, N, H, W, w.c2);
+  const bool planes = R.m->prec >= 1 && split_a_enabled() && w.c2.Bh != nullptr && w.mid >= 64 && !c2_wino;
   float* a1 = R.ws.get<float>((size_t)M * w.mid);  // fp32 or, with planes, hi|lo f16 halves
   float* r2 = R.ws.get<float>((size_t)M * w.cout);
   float2* rp2 = R.ws.get<float2>((size_t)M * (w.cout / seg));
@@ -1274,8 +1343,8 @@ static float* resblock(Run& R, const ResW& w, const SrcDesc& in, int mode, int N
   // The mid GroupNorm + GELU folded into conv2's halo staging (igemm_halo.h GNA) where conv2 runs
   // the halo conv and conv1 wrote whole-sample partials (no split-K slabs): no norm_kernel launch,
   // no hi / lo planes.  DMX_GN_FUSE=0 turns it off (the staged operand is the same either way).
-  const bool fuse1 = gn_fuse_enabled() && planes && !d1.fused && !R.m->debug &&
-                     halo_bn(R, w.mid, N, H, W, w.c2, EPI_STATS, true) > 0;
+  const bool fuse1 = gn_fuse_enabled() && !d1.fused && !R.m->debug &&
+                     ((planes && halo_bn(R, w.mid, N, H, W, w.c2, EPI_STATS, true) > 0) || c2_wino);
   int rr2;
   if (fuse1) {
     GnLoad g;
@@ -1500,6 +1569,9 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
   dmx_model* m = R.m;
   // embedding
   float* emb = R.ws.get<float>((size_t)N * m->hsum);
+  const bool has_cond = m->kind != DMX_UNET && in.vals != nullptr;
+  const int cond_rows = in.cond_rows > 0 ? in.cond_rows : N;
+  float* cnd = has_cond ? R.ws.get<float>((size_t)cond_rows * 256) : nullptr;
   if (!R.plan) {
     EmbedParams e;
     std::memset(&e, 0, sizeof(e));
@@ -1527,6 +1599,13 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
     e.hsum = m->hsum;
     e.out = emb;
     R.layer = "embed";
+    if (has_cond) {  // cond_mlp once per distinct condition row (the CFG halves share it)
+      R.begin("cond_emb_kernel", 2.0 * cond_rows * (24.0 * 256 + 256.0 * 256), 4.0 * (256.0 * 256 + 24.0 * 256));
+      cond_emb_kernel<<<cond_rows, 256, 0, R.st>>>(e, cnd);
+      R.end();
+      HIPCHK(hipGetLastError());
+      e.cnd = cnd;
+    }
     R.begin("embed_kernel", 2.0 * N * (24.0 * 256 + 256.0 * 256 + 256.0 * m->hsum), 4.0 * (256.0 * 256 + 256.0 * m->hsum));
     embed_kernel<<<dim3(N, cdiv(m->hsum, 256)), 256, 0, R.st>>>(e);
     R.end();
@@ -1563,13 +1642,15 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
     float* pooled = R.ws.get<float>(pool_el);
     const bool pool_planes = R.m->prec >= 1 && m->down[i].r0.c1.Bh != nullptr && !R.m->debug && cat_planes_enabled() &&
                              !(cat_planes_mode() == 2 && (halo_bn(R, cc, nb, nh, nw, m->down[i].r0.c1, EPI_STATS, true) > 0 ||
-                                                          halo_ms_bn_any(R, cc, nb, nh, nw, m->down[i].r0.c1)));
+                                                          halo_ms_bn_any(R, cc, nb, nh, nw, m->down[i].r0.c1))) &&
+                             !wino_any(R, cc, nb, nh, nw, m->down[i].r0.c1);
     _Float16* pool_h = pool_planes ? R.ws.get<_Float16>(2 * pool_el) : nullptr;
     _Float16* pool_l = pool_planes ? pool_h + pool_el : nullptr;
     prep<SRC_MAXPOOL>(R, mp, pooled, nb, nh, nw, "prep_kernel<2>", pool_h, pool_l);
     bool hp = false;
     float* h0 = resblock(R, m->down[i].r0, plain_src(pooled, cc), SRC_PLAIN, nb, nh, nw, true, nullptr, 0, 0, 0,
-                         pool_h, pool_l, m->down[i].r1.c1.Bh != nullptr, &hp);
+                         pool_h, pool_l, m->down[i].r1.c1.Bh != nullptr && !wino_any(R, cc, nb, nh, nw, m->down[i].r1.c1),
+                         &hp);
     R.layer = "down" + std::to_string(i + 1) + ".1";
     const _Float16* h0h = hp ? reinterpret_cast<const _Float16*>(h0) : nullptr;
     float* h1 = resblock(R, m->down[i].r1, plain_src(h0, cc), SRC_PLAIN, nb, nh, nw, false, emb, m->hsum,
@@ -1585,7 +1666,8 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
   for (int i = 0; i < m->nbot; ++i) {
     R.layer = "bot" + std::to_string(i + 1);
     bool hp = false;
-    const bool nxt = i + 1 < m->nbot && m->bot[i + 1].c1.Bh != nullptr;  // the last one feeds the upsample
+    const bool nxt = i + 1 < m->nbot && m->bot[i + 1].c1.Bh != nullptr &&  // the last one feeds the upsample
+                     !wino_any(R, m->bot[i].cout, N, ch, cw, m->bot[i + 1].c1);
     cur = resblock(R, m->bot[i], plain_src(cur, cc), SRC_PLAIN, N, ch, cw, false, nullptr, 0, 0, 0, cur_h, cur_l, nxt,
                    &hp);
     cc = m->bot[i].cout;
@@ -1611,7 +1693,8 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
     // the concat feeds conv1 (split GEMM: also as f16 planes) and the residual (fp32)
     const bool cat_planes = R.m->prec >= 1 && m->up[i].r0.c1.Bh != nullptr && !R.m->debug && cat_planes_enabled() &&
                             !(cat_planes_mode() == 2 && (halo_bn(R, u.C, N, sh[si], sw[si], m->up[i].r0.c1, EPI_STATS, true) > 0 ||
-                                                         halo_ms_bn_any(R, u.C, N, sh[si], sw[si], m->up[i].r0.c1)));
+                                                         halo_ms_bn_any(R, u.C, N, sh[si], sw[si], m->up[i].r0.c1))) &&
+                            !wino_any(R, u.C, N, sh[si], sw[si], m->up[i].r0.c1);
     _Float16* cat_h = cat_planes ? R.ws.get<_Float16>(2 * cat_el) : nullptr;
     _Float16* cat_l = cat_planes ? cat_h + cat_el : nullptr;
     prep<SRC_UPCAT>(R, u, cat, N, sh[si], sw[si], "prep_kernel<3>", cat_h, cat_l);
@@ -1619,10 +1702,11 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
     // r0's final GroupNorm + residual + GELU folded into r1's halo conv1 where that conv runs the
     // halo kernel (igemm_halo.h GNA = 2): one norm_kernel launch and the h0 round trip fewer
     GnLoad dly;
+    const bool r1_wino = wino_any(R, u.C, N, sh[si], sw[si], m->up[i].r1.c1);
     const bool try_defer = gn_fuse_enabled() && !R.m->debug && R.m->prec >= 1 &&
-                           halo_bn(R, u.C, N, sh[si], sw[si], m->up[i].r1.c1, EPI_STATS, true) > 0;
+                           (halo_bn(R, u.C, N, sh[si], sw[si], m->up[i].r1.c1, EPI_STATS, true) > 0 || r1_wino);
     float* h0 = resblock(R, m->up[i].r0, plain_src(cat, u.C), SRC_PLAIN, N, sh[si], sw[si], true, nullptr, 0, 0, 0,
-                         cat_h, cat_l, m->up[i].r1.c1.Bh != nullptr, &hp, try_defer ? &dly : nullptr);
+                         cat_h, cat_l, m->up[i].r1.c1.Bh != nullptr && !r1_wino, &hp, try_defer ? &dly : nullptr);
     R.layer = "up" + std::to_string(i + 1) + ".1";
     const _Float16* h0h = hp ? reinterpret_cast<const _Float16*>(h0) : nullptr;
     float* h1 = dly.rowpart != nullptr

@@ -81,15 +81,34 @@ static __global__ void wino_pack_kernel(const float* B, int kpad, int cin, int c
   }
 }
 
-template <int W, int GNA>
+// Geometry.  W = 32: a block is 8 output rows of one sample (4 tile rows x 16); W = 16: one whole
+// sample (8 x 8 tiles); W = 8: four whole samples (4 x 4 tiles each), their halos stacked at a pitch
+// of PS = 11 halo rows (the 11th row is padding).  Halo pixel (row, col) lives at float offset
+// (row * 2 + col % 2) * RP * 4 + (col / 2) * 20 + channel: even / odd columns in separate planes,
+// 20 floats (16 channels + 4 pad) per pixel, RP 16-byte units per plane row.  A fragment row (tile)
+// of lane fr then reads at (s * PS + 2 ty) * 8 RP + 5 tx units + const, and RP is chosen so that each
+// 16-lane group of ds_read_b128 ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32) hits 16 distinct
+// 16-byte bank slots: W = 32 (2 tile rows per 32 tiles) needs 4 RP = 0 mod 16 (RP = 88), W = 16
+// (4 tile rows) 4 RP = 8 mod 16 (RP = 46), W = 8 (2 samples x 4 tile rows, PS = 11) 2 RP = 4 mod 16
+// (RP = 26).
+// EPI = EPI_STATS: the conv output and its GroupNorm partials; EPI_PARTIAL (grid.z = K splits over
+// 16-channel chunks, P.g.ksplit chunks each): the split's transformed partial output to slab z,
+// reduced in split order by reduce_norm_kernel / splitk_reduce_kernel (the output transform is
+// linear, so transforming each split's partial sums and adding the pixels equals transforming the
+// total).
+template <int W, int GNA, int EPI = EPI_STATS>
 __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
-  static_assert(W == 32 || W == 16, "Winograd conv: image width 16 or 32");
+  static_assert(EPI == EPI_STATS || EPI == EPI_PARTIAL, "Winograd epilogues");
+  static_assert(W == 32 || W == 16 || W == 8, "Winograd conv: image width 8, 16 or 32");
   const IgemmParams& p = P.g;
-  constexpr int TW = W / 2;                 // tiles per tile row
-  constexpr int TR = 256 / W;               // output rows of the block (64 tiles)
-  constexpr int HR = TR + 2, HC = W + 2;    // halo rows / columns
-  constexpr int RP = W == 32 ? 88 : 46;     // parity-plane row pitch in 16-byte units (see header)
-  constexpr int HBUF = HR * 2 * RP * 4;     // floats per halo buffer
+  constexpr int TW = W / 2;                       // tiles per tile row
+  constexpr int SPB = W == 8 ? 4 : 1;             // samples per block
+  constexpr int TPS = 64 / SPB;                   // tiles per sample in the block
+  constexpr int HRS = (W == 32 ? 8 : W) + 2;      // halo rows per sample
+  constexpr int PS = W == 8 ? 11 : HRS;           // halo row pitch between stacked samples
+  constexpr int HR = SPB * PS, HC = W + 2;        // halo rows / columns
+  constexpr int RP = W == 32 ? 88 : W == 16 ? 46 : 26;  // parity-plane row pitch in 16-byte units
+  constexpr int HBUF = HR * 2 * RP * 4;           // floats per halo buffer
   constexpr int CK = 16;                    // channels per chunk
   constexpr int NPC = HR * HC * (CK / 4);   // float4 pieces per chunk
   constexpr int NPI = (NPC + 511) / 512;    // pieces per thread
@@ -105,8 +124,10 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   xcd_tile(mt, nt, bz);
   const int m0 = mt * 256;
   const int HW = p.H * W, C = p.src.C;
-  const int nsmp = m0 / HW, y0 = (m0 - nsmp * HW) / W;
-  const int nch = C / CK;
+  const int nsmp = m0 / HW, y0 = (m0 - nsmp * HW) / W;  // first sample of the block; W = 32: first row
+  const int nch_all = C / CK;
+  const int cbeg = EPI == EPI_PARTIAL ? bz * p.ksplit : 0;  // first chunk of this split
+  const int nch = EPI == EPI_PARTIAL ? min(p.ksplit, nch_all - cbeg) : nch_all;
 
   // ---- halo pieces of this thread: (halo pixel, 4-channel quad), global element offset (chunk 0)
   // or -1 (zero padding), LDS float offset
@@ -116,72 +137,84 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
     const int e = tid + 512 * k;
     const int h = e >> 2, q = e & 3;
     const int hy = h / HC, hx = h - hy * HC;
-    const int y = y0 + hy - 1, x = hx - 1;
-    const bool ok = e < NPC && y >= 0 && y < p.H && x >= 0 && x < W;
-    hoff[k] = ok ? (((nsmp * p.H + y) * W + x) * C + q * 4) : -1;
+    const int sh = hy / PS, ry = hy - sh * PS;  // stacked sample, halo row inside it
+    const int y = y0 + ry - 1, x = hx - 1;
+    const bool ok = e < NPC && ry < HRS && y >= 0 && y < p.H && x >= 0 && x < W;
+    hoff[k] = ok ? ((((nsmp + sh) * p.H + y) * W + x) * C + q * 4) : -1;
     // pieces past the halo store to a scratch slot of their own (no divergent branch around the store)
     hls[k] = e < NPC ? ((hy * 2 + (hx & 1)) * RP * 4 + (hx >> 1) * 20 + q * 4) : 2 * HBUF + (tid & 255) * 4;
   }
   const __amdgpu_buffer_rsrc_t rA = rsrc_of(p.src.src0, P.a_bytes);
   const __amdgpu_buffer_rsrc_t rRes = rsrc_of(GNA == 2 ? (const void*)P.gn_res : (const void*)p.src.src0, P.a_bytes);
 
-  // ---- GroupNorm(1, C) statistics of sample nsmp (as igemm_halo_kernel / norm_kernel reduce them)
-  float2 gst = make_float2(0.f, 0.f);
+  // ---- GroupNorm(1, C) statistics of the block's samples (as igemm_halo_kernel / norm_kernel reduce
+  // them: 256 threads sum strided partials in double, wave shuffle tree, ((w0 + w1) + (w2 + w3)))
+  __shared__ float2 gst_s[SPB];
   if constexpr (GNA) {
     __shared__ double gr1[4], gr2[4];
-    __shared__ float2 gst_s;
-    if (tid < 256) {
-      const float2* rp = P.gn_rowpart + (size_t)nsmp * P.gn_cnt;
-      double s1 = 0.0, s2 = 0.0;
-      for (int i = tid; i < P.gn_cnt; i += 256) {
-        const float2 q = rp[i];
-        s1 += (double)q.x;
-        s2 += (double)q.y;
-      }
+    for (int sp = 0; sp < SPB; ++sp) {
+      if (tid < 256) {
+        const float2* rp = P.gn_rowpart + (size_t)(nsmp + sp) * P.gn_cnt;
+        double s1 = 0.0, s2 = 0.0;
+        for (int i = tid; i < P.gn_cnt; i += 256) {
+          const float2 q = rp[i];
+          s1 += (double)q.x;
+          s2 += (double)q.y;
+        }
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        s1 += __shfl_xor(s1, o, 64);
-        s2 += __shfl_xor(s2, o, 64);
+        for (int o = 32; o > 0; o >>= 1) {
+          s1 += __shfl_xor(s1, o, 64);
+          s2 += __shfl_xor(s2, o, 64);
+        }
+        if ((tid & 63) == 0) {
+          gr1[tid >> 6] = s1;
+          gr2[tid >> 6] = s2;
+        }
       }
-      if ((tid & 63) == 0) {
-        gr1[tid >> 6] = s1;
-        gr2[tid >> 6] = s2;
+      __syncthreads();
+      if (tid == 0) {
+        const double cntd = (double)HW * (double)C;
+        const double mean = ((gr1[0] + gr1[1]) + (gr1[2] + gr1[3])) / cntd;
+        double var = ((gr2[0] + gr2[1]) + (gr2[2] + gr2[3])) / cntd - mean * mean;
+        var = var < 0.0 ? 0.0 : var;
+        gst_s[sp] = make_float2((float)mean, (float)(1.0 / sqrt(var + 1e-5)));
       }
+      __syncthreads();
     }
-    __syncthreads();
-    if (tid == 0) {
-      const double cntd = (double)HW * (double)C;
-      const double mean = ((gr1[0] + gr1[1]) + (gr1[2] + gr1[3])) / cntd;
-      double var = ((gr2[0] + gr2[1]) + (gr2[2] + gr2[3])) / cntd - mean * mean;
-      var = var < 0.0 ? 0.0 : var;
-      gst_s = make_float2((float)mean, (float)(1.0 / sqrt(var + 1e-5)));
-    }
-    __syncthreads();
-    gst = gst_s;
   }
 
   floatx4 ha[NPI];
   floatx4 hr[GNA == 2 ? NPI : 1];
-  floatx4 ggam = {0.f, 0.f, 0.f, 0.f}, gbet = {0.f, 0.f, 0.f, 0.f};
-  auto load_halo = [&](int c) {
-    if constexpr (GNA) {  // every piece of this thread holds the same channel quad (512 % 4 == 0)
-      const int ch = c * CK + (tid & 3) * 4;
-      ggam = ld4(P.gn_gamma + ch);
-      gbet = ld4(P.gn_beta + ch);
+  // GroupNorm affine of all C channels in LDS (read per staged quad: no registers held across the chunk)
+  __shared__ __attribute__((aligned(16))) float gaff[GNA ? 2 * 512 : 4];
+  if constexpr (GNA) {
+    for (int i = tid; i < C; i += 512) {
+      gaff[i] = P.gn_gamma[i];
+      gaff[512 + i] = P.gn_beta[i];
     }
+    __syncthreads();
+  }
+  auto load_halo = [&](int c) {
 #pragma unroll
     for (int k = 0; k < NPI; ++k) {
-      const int off = hoff[k] >= 0 ? (hoff[k] + c * CK) * 4 : kOOB;
+      const int off = hoff[k] >= 0 ? (hoff[k] + (cbeg + c) * CK) * 4 : kOOB;
       ha[k] = bload_f4(rA, off, 0);
       if constexpr (GNA == 2) hr[k] = bload_f4(rRes, off, 0);
     }
   };
-  auto store_halo = [&](int buf) {
+  auto store_halo = [&](int buf, int c) {
     float* hb = lds + buf * HBUF;
+    floatx4 ggam = {0.f, 0.f, 0.f, 0.f}, gbet = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (GNA) {  // every piece of this thread holds the same channel quad (512 % 4 == 0)
+      const int ch = (cbeg + c) * CK + (tid & 3) * 4;
+      ggam = *reinterpret_cast<const floatx4*>(&gaff[ch]);
+      gbet = *reinterpret_cast<const floatx4*>(&gaff[512 + ch]);
+    }
 #pragma unroll
     for (int k = 0; k < NPI; ++k) {
       floatx4 v = ha[k];
       if constexpr (GNA) {  // GroupNorm (+ residual) + GELU of the raw source; zero padding stays zero
+        const float2 gst = gst_s[SPB == 1 ? 0 : min(((tid + 512 * k) >> 2) / HC / PS, SPB - 1)];
         v = gn_apply4v(v, gst, ggam, gbet, GNA == 1 ? 1 : 0);
         if constexpr (GNA == 2) {
 #pragma unroll
@@ -207,8 +240,8 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   int cnext = 0;  // chunk whose fragments load_b(.., -1) fetches
   auto load_b = [&](int q, int n, int c) {
     const int cc = c < 0 ? cnext : c;
-    bh[q][n] = bload_h8(rUh, voff, ub[q][n] + cc * 1024);
-    bl[q][n] = bload_h8(rUl, voff, ub[q][n] + cc * 1024);
+    bh[q][n] = bload_h8(rUh, voff, ub[q][n] + (cbeg + cc) * 1024);
+    bl[q][n] = bload_h8(rUl, voff, ub[q][n] + (cbeg + cc) * 1024);
   };
 
   // ---- A fragments: rows (Bᵀ row wi) and columns (B columns of positions 2jp, 2jp + 1)
@@ -225,42 +258,36 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   int tb[2];
 #pragma unroll
   for (int mb = 0; mb < 2; ++mb) {
-    const int t = 32 * mb + fr, ty = t / TW, tx = t - ty * TW;
-    tb[mb] = ty * 16 * RP + tx * 20 + 8 * fh;
+    const int t = 32 * mb + fr, st = t / TPS, tt = t - st * TPS, ty = tt / TW, tx = tt - ty * TW;
+    tb[mb] = (st * PS + 2 * ty) * 8 * RP + tx * 20 + 8 * fh;
   }
   half8 ah[2], al[2];  // [position] of the current m tile
   auto build = [&](int buf, int mb) {
-    const float* hb = lds + buf * HBUF;
-    {
-      floatx4 T[3][2];
+    const float* hb = lds + buf * HBUF + tb[mb];
+    unsigned vh[2][4], vl[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // channels 4h .. 4h + 3 of the lane's eight (fewer live registers)
+      floatx4 T[3];
       const int oc[3] = {op, oq, os};
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        const float* pa = hb + tb[mb] + oa + oc[k];
-        const float* pb = hb + tb[mb] + ob + oc[k];
+        const floatx4 da = *reinterpret_cast<const floatx4*>(hb + oa + oc[k] + 4 * h);
+        const floatx4 db = *reinterpret_cast<const floatx4*>(hb + ob + oc[k] + 4 * h);
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const floatx4 da = *reinterpret_cast<const floatx4*>(pa + 4 * h);
-          const floatx4 db = *reinterpret_cast<const floatx4*>(pb + 4 * h);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) T[k][h][e] = fmaf(db[e], sr, da[e]);
-        }
+        for (int e = 0; e < 4; ++e) T[k][e] = fmaf(db[e], sr, da[e]);
       }
-      unsigned vh[2][4], vl[2][4];
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int e = 0; e < 4; e += 2) {
-          const float a0 = T[0][h][e] - T[1][h][e], a1 = T[0][h][e + 1] - T[1][h][e + 1];
-          const float b0 = fmaf(T[2][h][e], sb, T[1][h][e]), b1 = fmaf(T[2][h][e + 1], sb, T[1][h][e + 1]);
-          split2u(a0, a1, vh[0][2 * h + e / 2], vl[0][2 * h + e / 2]);
-          split2u(b0, b1, vh[1][2 * h + e / 2], vl[1][2 * h + e / 2]);
-        }
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        ah[q] = __builtin_bit_cast(half8, (u32x4){vh[q][0], vh[q][1], vh[q][2], vh[q][3]});
-        al[q] = __builtin_bit_cast(half8, (u32x4){vl[q][0], vl[q][1], vl[q][2], vl[q][3]});
+      for (int e = 0; e < 4; e += 2) {
+        const float a0 = T[0][e] - T[1][e], a1 = T[0][e + 1] - T[1][e + 1];
+        const float b0 = fmaf(T[2][e], sb, T[1][e]), b1 = fmaf(T[2][e + 1], sb, T[1][e + 1]);
+        split2u(a0, a1, vh[0][2 * h + e / 2], vl[0][2 * h + e / 2]);
+        split2u(b0, b1, vh[1][2 * h + e / 2], vl[1][2 * h + e / 2]);
       }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      ah[q] = __builtin_bit_cast(half8, (u32x4){vh[q][0], vh[q][1], vh[q][2], vh[q][3]});
+      al[q] = __builtin_bit_cast(half8, (u32x4){vl[q][0], vl[q][1], vl[q][2], vl[q][3]});
     }
   };
 
@@ -280,15 +307,21 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   for (int q = 0; q < 2; ++q)
 #pragma unroll
     for (int n = 0; n < 2; ++n) load_b(q, n, 0);
-  store_halo(0);
+  store_halo(0, 0);
   load_halo(min(1, nch - 1));
   __syncthreads();
 
-  // Per chunk: next halo to LDS (its registers free before the A build), m tile 0's A fragments and
-  // MFMAs, m tile 1's, with chunk c + 2's halo loads issued between the two; every U fragment is
-  // reloaded for chunk c + 1 right after its last MFMA of chunk c.  Register peak: 128 accumulators +
-  // 32 U + one m tile's A fragments + the build temporaries / the halo pieces in flight.
-  auto mfmas = [&](int i, bool last) {
+  // Per chunk c (halo buffers alternate; U fragments rolling in registers):
+  //   store chunk c + 1's halo (registers loaded one chunk earlier) -> buffer (c + 1) & 1, issue chunk
+  //   c + 2's halo loads; A fragments of m tile 0 + its 12 MFMAs; A fragments of m tile 1; BARRIER;
+  //   m tile 1's 12 MFMAs, each U fragment reloaded for chunk c + 1 right after its last use.
+  // The barrier sits before the last MFMA group: every wave has finished reading buffer c & 1 (its
+  // builds) and writing buffer (c + 1) & 1, so the next chunk may overwrite / read them, and the
+  // MFMAs issued after it overlap the co-resident wave's halo store and A build.  Global loads are
+  // pinned by sched barriers (only VALU / SALU / LDS ops may move across), so the compiler cannot
+  // sink them to the loop end, and they are issued unconditionally (chunk indices clamped; the loads
+  // of the last iterations are never used) so the vector-memory counter waits stay exact.
+  auto mfmas = [&](int i, bool reload) {
 #pragma unroll
     for (int q = 0; q < 2; ++q)
 #pragma unroll
@@ -296,24 +329,33 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
         acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[q], bh[q][n], acc[q][i][n], 0, 0, 0);
         acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[q], bl[q][n], acc[q][i][n], 0, 0, 0);
         acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[q], bh[q][n], acc[q][i][n], 0, 0, 0);
-        if (last) load_b(q, n, -1);  // (always: a static load sequence keeps the vmcnt waits exact)
+        if (reload) {
+          load_b(q, n, -1);
+          __builtin_amdgcn_sched_barrier(0x0086);
+        }
       }
   };
-  // Every global load is issued unconditionally (chunk indices clamped to the last chunk; the extra
-  // loads of the final iterations are never used) so the vector-memory counter sequence is the same
-  // on every iteration and each wait covers exactly the loads it needs.
   for (int c = 0; c < nch; ++c) {
-    store_halo((c + 1) & 1);  // buffer (c + 1) & 1 was last read by chunk c - 1 (c + 1 = nch: unused)
+    store_halo((c + 1) & 1, min(c + 1, nch - 1));  // c + 1 = nch: an unused store of the last chunk
+    constexpr bool LATE = GNA == 2 || (W != 32 && GNA == 1);  // (register pressure: after m tile 0)
+    if constexpr (!LATE) {
+      load_halo(min(c + 2, nch - 1));
+      __builtin_amdgcn_sched_barrier(0x0086);
+    }
     build(c & 1, 0);
     mfmas(0, false);
+    if constexpr (LATE) {
+      load_halo(min(c + 2, nch - 1));
+      __builtin_amdgcn_sched_barrier(0x0086);
+    }
     build(c & 1, 1);
-    load_halo(min(c + 2, nch - 1));
     cnext = min(c + 1, nch - 1);
-    mfmas(1, true);
     __syncthreads();
+    mfmas(1, true);
   }
 
   // ---- epilogue: Aᵀ M A per tile, four passes of 32 tiles x 32 channels through LDS
+  __syncthreads();  // (the halo buffers become the epilogue's staging area)
   const int HW16 = HW / 16, nseg = p.Cout / 32;
   const int tile0 = (m0 - nsmp * HW) / 4;  // first tile of the block inside its sample
   const int cc = tid & 31, tp = tid >> 5;  // output task: channel cc, tiles 2 tp, 2 tp + 1
@@ -340,7 +382,9 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
         m[xi][1] = v.y;
       }
       const int col = 64 * nt + 32 * n + cc;
-      const float bias = p.bias != nullptr ? p.bias[col] : 0.f;
+      // (split partials carry no bias: the slab reduction adds it once)
+      const float bias = (EPI == EPI_STATS && p.bias != nullptr) ? p.bias[col] : 0.f;
+      float* dst = EPI == EPI_PARTIAL ? p.partial + (size_t)bz * p.M * p.Cout : p.out;
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -350,27 +394,29 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
           z[i][0] = (m[4 * i][e] + m[4 * i + 1][e]) + m[4 * i + 2][e];
           z[i][1] = (m[4 * i + 1][e] - m[4 * i + 2][e]) - m[4 * i + 3][e];
         }
-        const int t = 32 * mb + 2 * tp + e, ty = t / TW, tx = t - ty * TW;
+        const int t = 32 * mb + 2 * tp + e, st = t / TPS, tt = t - st * TPS, ty = tt / TW, tx = tt - ty * TW;
 #pragma unroll
         for (int r = 0; r < 2; ++r)
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
             const float y = (r == 0 ? (z[0][s] + z[1][s]) + z[2][s] : (z[1][s] - z[2][s]) - z[3][s]) + bias;
             const int oy = y0 + 2 * ty + r, ox = 2 * tx + s;
-            p.out[(((size_t)nsmp * p.H + oy) * W + ox) * p.Cout + col] = y;
+            dst[(((size_t)(nsmp + st) * p.H + oy) * W + ox) * p.Cout + col] = y;
             s1 += y;
             s2 += y * y;
           }
       }
       // partial of 4 tiles (16 pixels) x 32 channels = this wave's 64 lanes
+      if constexpr (EPI == EPI_STATS) {
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        s1 += __shfl_xor(s1, o, 64);
-        s2 += __shfl_xor(s2, o, 64);
+        for (int o = 1; o < 64; o <<= 1) {
+          s1 += __shfl_xor(s1, o, 64);
+          s2 += __shfl_xor(s2, o, 64);
+        }
       }
-      if (lane == 0) {
-        const int g = (tile0 + 32 * mb + 4 * wid) / 4;
-        p.rowpart[((size_t)nsmp * HW16 + g) * nseg + 2 * nt + n] = make_float2(s1, s2);
+      if (EPI == EPI_STATS && lane == 0) {  // the wave's 4 tiles: one tile row of one sample
+        const int t = 32 * mb + 4 * wid, st = t / TPS, g = (tile0 + t - st * TPS) / 4;
+        p.rowpart[((size_t)(nsmp + st) * HW16 + g) * nseg + 2 * nt + n] = make_float2(s1, s2);
       }
       __syncthreads();
     }

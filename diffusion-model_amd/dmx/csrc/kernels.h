@@ -39,7 +39,34 @@ struct EmbedParams {
   int hsum;
   float* out;                  // [n][hsum]
   int64_t* t_next;             // sample-loop graphs (scalar t): block (0, 0) stores t - 1 here
+  const float* cnd;            // [cond_rows][256] cond_mlp outputs (cond_emb_kernel), or null: inline
 };
+
+// cond_mlp([vals, mask]) (models/unet_cond.py:125-129, 187-190) once per DISTINCT condition row: the
+// CFG halves and every step of a sample loop share it (t-independent), so embed_kernel's blocks
+// (N samples x head slices) read it instead of each recomputing the 256 x 256 product.  Same
+// arithmetic and summation order as the inline path: the sums are bit-identical.
+static __global__ __launch_bounds__(256) void cond_emb_kernel(const EmbedParams p, float* cnd) {
+  __shared__ float h[256], in24[24];
+  const int row = blockIdx.x, k = threadIdx.x;
+  if (k < 12) in24[k] = p.vals[row * 12 + k];
+  else if (k < 24) in24[k] = p.mask[row * 12 + (k - 12)];
+  __syncthreads();
+  float a = p.b0[k];
+#pragma unroll
+  for (int j = 0; j < 24; ++j) a += p.w0[k * 24 + j] * in24[j];
+  h[k] = silu(a);
+  __syncthreads();
+  float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f;
+#pragma unroll
+  for (int j = 0; j < 256; j += 4) {
+    c0 += p.w2t[(j + 0) * 256 + k] * h[j + 0];
+    c1 += p.w2t[(j + 1) * 256 + k] * h[j + 1];
+    c2 += p.w2t[(j + 2) * 256 + k] * h[j + 2];
+    c3 += p.w2t[(j + 3) * 256 + k] * h[j + 3];
+  }
+  cnd[row * 256 + k] = p.b2[k] + ((c0 + c1) + (c2 + c3));
+}
 
 // grid = (n, parts): every block recomputes the sample's 256-wide embedding (cheap) and
 // produces its 1/parts slice of the concatenated head outputs (coalesced weight reads).
@@ -58,7 +85,9 @@ static __global__ __launch_bounds__(256) void embed_kernel(const EmbedParams p) 
     yy = yy < 0 ? 0 : (yy >= p.ncls ? p.ncls - 1 : yy);
     v += p.class_emb[yy * 256 + k];
   }
-  if (p.vals != nullptr) {
+  if (p.cnd != nullptr) {
+    v += p.cnd[(n % p.cond_rows) * 256 + k];
+  } else if (p.vals != nullptr) {
     const int row = n % p.cond_rows;
     if (k < 12) in24[k] = p.vals[row * 12 + k];
     else if (k < 24) in24[k] = p.mask[row * 12 + (k - 12)];
@@ -95,6 +124,80 @@ static __global__ __launch_bounds__(256) void embed_kernel(const EmbedParams p) 
     }
     p.out[(size_t)n * p.hsum + o] = p.bh[o] + ((a0 + a1) + (a2 + a3));
   }
+}
+
+// ---------------------------------------------------------------------------
+// inc's first conv (models/unet_cond.py:17, Conv2d(in_ch, 64, 3, padding=1, bias=False)) on the NCHW
+// network input: K = 9 taps x <= 4 channels is far too thin for a GEMM (the implicit GEMM padded it
+// to 64 and paid a global round trip per 16-deep K step), so it runs as a direct fp32 conv: a block
+// owns 32 output pixels (one image row, W % 32 == 0) x 64 channels, thread (pixel, 8-channel group)
+// accumulates its 36 products per channel in fixed (tap, channel) order with fp32 FMAs (exact fp32
+// semantics in every precision mode), the 64 x 36 weights staged in LDS.  Output NHWC fp32 plus the
+// GroupNorm (sum, sum of squares) partial of each (32 pixels, 32 channels) group — the layout
+// igemm_epilogue writes (rgrp = 32, seg = 32).
+// ---------------------------------------------------------------------------
+struct ConvInParams {
+  const float* x;      // NCHW [n][creal][H][W]
+  int creal, n_mod;    // channels present; sample index modulo n_mod (0: none)
+  float scale;         // divide the input by scale (1: identity)
+  const float* B;      // packed [npad][kpad], k = tap * cin + c
+  int cin, kpad;
+  float* out;          // NHWC [n][H][W][64]
+  float2* rowpart;     // [n][HW / 32][2]
+  int H, W;
+};
+static __global__ __launch_bounds__(256) void conv_in_kernel(const ConvInParams p) {
+  __shared__ float ws[64][37];
+  __shared__ float2 red[4];
+  const int tid = threadIdx.x, px = tid & 31, g = tid >> 5;
+  for (int i = tid; i < 64 * 36; i += 256) {
+    const int co = i / 36, k = i - co * 36, tap = k >> 2, c = k & 3;
+    ws[co][k] = c < p.cin ? p.B[(size_t)co * p.kpad + tap * p.cin + c] : 0.f;
+  }
+  const int HW = p.H * p.W;
+  const int m0 = blockIdx.x * 32;
+  const int n = m0 / HW, r = m0 - n * HW, y = r / p.W, x = r - y * p.W + px;
+  const int ns = p.n_mod ? n % p.n_mod : n;
+  float in[36];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int iy = y + tap / 3 - 1, ix = x + tap % 3 - 1;
+    const bool ok = iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float v = (ok && c < p.creal) ? p.x[((size_t)ns * p.creal + c) * HW + (size_t)iy * p.W + ix] : 0.f;
+      in[tap * 4 + c] = p.scale != 1.f ? v / p.scale : v;
+    }
+  }
+  __syncthreads();
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < 36; ++k) a = fmaf(ws[8 * g + j][k], in[k], a);
+    acc[j] = a;
+  }
+  float* o = p.out + ((size_t)m0 + px) * 64 + 8 * g;
+  *reinterpret_cast<floatx4*>(o) = floatx4{acc[0], acc[1], acc[2], acc[3]};
+  *reinterpret_cast<floatx4*>(o + 4) = floatx4{acc[4], acc[5], acc[6], acc[7]};
+  // GroupNorm partials: segment s = channels 32 s .. + 31 = groups g in [4 s, 4 s + 3] = waves 2 s, 2 s + 1
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    s1 += acc[j];
+    s2 += acc[j] * acc[j];
+  }
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    s1 += __shfl_xor(s1, off, 64);
+    s2 += __shfl_xor(s2, off, 64);
+  }
+  if ((tid & 63) == 0) red[tid >> 6] = make_float2(s1, s2);
+  __syncthreads();
+  if (tid < 2)
+    p.rowpart[((size_t)n * (HW / 32) + r / 32) * 2 + tid] =
+        make_float2(red[2 * tid].x + red[2 * tid + 1].x, red[2 * tid].y + red[2 * tid + 1].y);
 }
 
 // ---------------------------------------------------------------------------

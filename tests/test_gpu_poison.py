@@ -47,6 +47,17 @@ for hw in (16, 28):
                 nm.step(x[s:e].contiguous(), o, tt[s:e], y[s:e], 0, vals[s:e].contiguous(), mask[s:e].contiguous(),
                         3.0, tables, noise[s:e].contiguous())
                 out[f"step{hw}_{prec}_{s}_{e}"] = o.cpu()
+# the benchmark shape (B = 64 CFG, 32 x 32): the large-grid kernels only this batch reaches
+# (Winograd F(2x2, 3x3) convs at 16 x 16 / 32 x 32, igemm_wino.h) under the same poison check
+Bb = 64
+xb = torch.randn((Bb, 4, 32, 32), generator=g).to(dev)
+nb = torch.randn((Bb, 4, 32, 32), generator=g).to(dev)
+vb = torch.rand((Bb, 12), generator=g).to(dev)
+mb = (torch.rand((Bb, 12), generator=g) > 0.3).float().to(dev)
+yb = torch.tensor([1 + i % 3 for i in range(Bb)], device=dev)
+ob = torch.empty_like(xb)
+nm.step(xb, ob, torch.full((Bb,), 3, dtype=torch.long, device=dev), yb, 0, vb, mb, 3.0, tables, nb)
+out["step32_b64_x3"] = ob.cpu()
 m.train()
 x = torch.randn((2, 4, 28, 28), generator=g).to(dev)
 t = torch.tensor([17, 900], device=dev)
