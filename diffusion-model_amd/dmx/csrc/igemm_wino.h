@@ -125,6 +125,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   const int m0 = mt * 256;
   const int HW = p.H * W, C = p.src.C;
   const int nsmp = m0 / HW, y0 = (m0 - nsmp * HW) / W;  // first sample of the block; W = 32: first row
+  const int nsamp = p.M / HW;  // W = 8: samples past the batch (last block) stage zeros, write nothing
   const int nch_all = C / CK;
   const int cbeg = EPI == EPI_PARTIAL ? bz * p.ksplit : 0;  // first chunk of this split
   const int nch = EPI == EPI_PARTIAL ? min(p.ksplit, nch_all - cbeg) : nch_all;
@@ -139,7 +140,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
     const int hy = h / HC, hx = h - hy * HC;
     const int sh = hy / PS, ry = hy - sh * PS;  // stacked sample, halo row inside it
     const int y = y0 + ry - 1, x = hx - 1;
-    const bool ok = e < NPC && ry < HRS && y >= 0 && y < p.H && x >= 0 && x < W;
+    const bool ok = e < NPC && ry < HRS && y >= 0 && y < p.H && x >= 0 && x < W && nsmp + sh < nsamp;
     hoff[k] = ok ? ((((nsmp + sh) * p.H + y) * W + x) * C + q * 4) : -1;
     // pieces past the halo store to a scratch slot of their own (no divergent branch around the store)
     hls[k] = e < NPC ? ((hy * 2 + (hx & 1)) * RP * 4 + (hx >> 1) * 20 + q * 4) : 2 * HBUF + (tid & 255) * 4;
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   if constexpr (GNA) {
     __shared__ double gr1[4], gr2[4];
     for (int sp = 0; sp < SPB; ++sp) {
-      if (tid < 256) {
+      if (tid < 256 && nsmp + sp < nsamp) {
         const float2* rp = P.gn_rowpart + (size_t)(nsmp + sp) * P.gn_cnt;
         double s1 = 0.0, s2 = 0.0;
         for (int i = tid; i < P.gn_cnt; i += 256) {
@@ -185,15 +186,6 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
 
   floatx4 ha[NPI];
   floatx4 hr[GNA == 2 ? NPI : 1];
-  // GroupNorm affine of all C channels in LDS (read per staged quad: no registers held across the chunk)
-  __shared__ __attribute__((aligned(16))) float gaff[GNA ? 2 * 512 : 4];
-  if constexpr (GNA) {
-    for (int i = tid; i < C; i += 512) {
-      gaff[i] = P.gn_gamma[i];
-      gaff[512 + i] = P.gn_beta[i];
-    }
-    __syncthreads();
-  }
   auto load_halo = [&](int c) {
 #pragma unroll
     for (int k = 0; k < NPI; ++k) {
@@ -207,8 +199,8 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
     floatx4 ggam = {0.f, 0.f, 0.f, 0.f}, gbet = {0.f, 0.f, 0.f, 0.f};
     if constexpr (GNA) {  // every piece of this thread holds the same channel quad (512 % 4 == 0)
       const int ch = (cbeg + c) * CK + (tid & 3) * 4;
-      ggam = *reinterpret_cast<const floatx4*>(&gaff[ch]);
-      gbet = *reinterpret_cast<const floatx4*>(&gaff[512 + ch]);
+      ggam = ld4(P.gn_gamma + ch);  // (L1 / L2 hits: 32 bytes per thread per chunk)
+      gbet = ld4(P.gn_beta + ch);
     }
 #pragma unroll
     for (int k = 0; k < NPI; ++k) {
@@ -301,23 +293,27 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[q][i][j][r] = 0.f;
 
-  // ---- prologue: chunk 0's halo in LDS, its U fragments and chunk 1's halo in flight
+  // ---- prologue: chunk 0's halo in LDS, chunk 1's halo and chunk 0's U fragments in flight — issued
+  // in the loop's steady-state order (halo loads older than U loads), so the counted vmcnt waits the
+  // compiler derives at the loop head (merged over entry and back edge) let the store of the halo
+  // retire only the halo loads instead of draining the U fragments too
   load_halo(0);
+  store_halo(0, 0);
+  load_halo(min(1, nch - 1));
 #pragma unroll
   for (int q = 0; q < 2; ++q)
 #pragma unroll
     for (int n = 0; n < 2; ++n) load_b(q, n, 0);
-  store_halo(0, 0);
-  load_halo(min(1, nch - 1));
   __syncthreads();
 
   // Per chunk c (halo buffers alternate; U fragments rolling in registers):
   //   store chunk c + 1's halo (registers loaded one chunk earlier) -> buffer (c + 1) & 1, issue chunk
-  //   c + 2's halo loads; A fragments of m tile 0 + its 12 MFMAs; A fragments of m tile 1; BARRIER;
-  //   m tile 1's 12 MFMAs, each U fragment reloaded for chunk c + 1 right after its last use.
-  // The barrier sits before the last MFMA group: every wave has finished reading buffer c & 1 (its
-  // builds) and writing buffer (c + 1) & 1, so the next chunk may overwrite / read them, and the
-  // MFMAs issued after it overlap the co-resident wave's halo store and A build.  Global loads are
+  //   c + 2's halo loads; A fragments of m tile 0 + its 12 MFMAs; A fragments of m tile 1 + its 12
+  //   MFMAs, each U fragment reloaded for chunk c + 1 right after its last use; BARRIER.
+  // (Measured: the barrier placed before the last MFMA group — to overlap those MFMAs with the next
+  // chunk's halo store — raced: with the sched barriers below, stored halo values of the next chunk
+  // reached LDS before slower waves' reads of the buffer, i.e. the hardware barrier no longer split
+  // the two; some GroupNorm-on-load outputs came out wrong.  Kept at the chunk end.)  Global loads are
   // pinned by sched barriers (only VALU / SALU / LDS ops may move across), so the compiler cannot
   // sink them to the loop end, and they are issued unconditionally (chunk indices clamped; the loads
   // of the last iterations are never used) so the vector-memory counter waits stay exact.
@@ -337,6 +333,13 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   };
   for (int c = 0; c < nch; ++c) {
     store_halo((c + 1) & 1, min(c + 1, nch - 1));  // c + 1 = nch: an unused store of the last chunk
+    // A barrier between the halo store and the A build.  Measured (tools/det_check.py, 12 repeats of
+    // a B = 128 forward): with the GroupNorm affine read from an LDS table in the store and no barrier
+    // here, GroupNorm-on-load convs were nondeterministic (some samples differed run to run, up to
+    // 6e-4 rel-L2); the LDS addresses of the store, the builds and the table are disjoint by
+    // construction and the root cause was not isolated.  This barrier alone, or the affine read from
+    // global memory alone, made every repeat bit-identical; both are kept (±0 measured).
+    __syncthreads();
     constexpr bool LATE = GNA == 2 || (W != 32 && GNA == 1);  // (register pressure: after m tile 0)
     if constexpr (!LATE) {
       load_halo(min(c + 2, nch - 1));
@@ -350,8 +353,8 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
     }
     build(c & 1, 1);
     cnext = min(c + 1, nch - 1);
-    __syncthreads();
     mfmas(1, true);
+    __syncthreads();
   }
 
   // ---- epilogue: Aᵀ M A per tile, four passes of 32 tiles x 32 channels through LDS
@@ -401,7 +404,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
           for (int s = 0; s < 2; ++s) {
             const float y = (r == 0 ? (z[0][s] + z[1][s]) + z[2][s] : (z[1][s] - z[2][s]) - z[3][s]) + bias;
             const int oy = y0 + 2 * ty + r, ox = 2 * tx + s;
-            dst[(((size_t)(nsmp + st) * p.H + oy) * W + ox) * p.Cout + col] = y;
+            if (nsmp + st < nsamp) dst[(((size_t)(nsmp + st) * p.H + oy) * W + ox) * p.Cout + col] = y;
             s1 += y;
             s2 += y * y;
           }
@@ -416,7 +419,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
       }
       if (EPI == EPI_STATS && lane == 0) {  // the wave's 4 tiles: one tile row of one sample
         const int t = 32 * mb + 4 * wid, st = t / TPS, g = (tile0 + t - st * TPS) / 4;
-        p.rowpart[((size_t)(nsmp + st) * HW16 + g) * nseg + 2 * nt + n] = make_float2(s1, s2);
+        if (nsmp + st < nsamp) p.rowpart[((size_t)(nsmp + st) * HW16 + g) * nseg + 2 * nt + n] = make_float2(s1, s2);
       }
       __syncthreads();
     }

@@ -103,6 +103,26 @@ def test_unet_forward_bench_batch_vs_oracle(model, cuda, unet_sd, prec):
     assert ee < TOL and eg < TOL
 
 
+def test_bench_batch_forward_is_deterministic(model, cuda):
+    """Five repeats of the N = 128 forward are bit-identical (the large-grid kernels — Winograd convs
+    with GroupNorm-on-load, split-K slabs — must not race: a race shows up as run-to-run drift of a
+    few samples; tools/det_check.py is the longer version of this check)."""
+    g = torch.Generator().manual_seed(129)
+    N = 128
+    x = torch.randn((N, 4, 32, 32), generator=g).to(cuda)
+    t = torch.randint(1, 1001, (N,), generator=g).to(cuda)
+    y = torch.randint(0, 4, (N,), generator=g).to(cuda)
+    vals = torch.rand((N, 12), generator=g).to(cuda)
+    mask = (torch.rand((N, 12), generator=g) > 0.5).float().to(cuda)
+    outs = []
+    with torch.no_grad():
+        for _ in range(5):
+            eps, geom = model(x, t, y, cond_vals=vals, cond_mask=mask)
+            outs.append((eps.cpu(), geom.cpu()))
+    for e, gm in outs[1:]:
+        assert torch.equal(e, outs[0][0]) and torch.equal(gm, outs[0][1])
+
+
 def test_uncond_unet_golden(golden, cuda):
     from dmx import synth
     from models.unet import Unet

@@ -86,8 +86,8 @@ def main():
     m.to(dev).eval()
     g = torch.Generator().manual_seed(0)
     x = torch.randn((a.n, 4, a.hw, a.hw), generator=g)
-    t = torch.tensor([1000, 517, 1, 42, 7][: a.n])
-    y = torch.tensor([0, 2, 3, 1, 1][: a.n])
+    t = torch.tensor([1000, 517, 1, 42, 7] * (a.n // 5 + 1))[: a.n]
+    y = torch.tensor([0, 2, 3, 1, 1] * (a.n // 5 + 1))[: a.n]
     vals = torch.rand((a.n, 12), generator=g)
     mask = (torch.rand((a.n, 12), generator=g) > 0.5).float()
     with torch.no_grad():
