@@ -845,11 +845,18 @@ struct GnLoad {
   const float* res = nullptr;       // non-null: GELU(res + GroupNorm(x)) (residual ResBlock output)
 };
 
+// Batch the tiling / split-K decisions are taken for: the VAE decoder's per-sample tile (Run::tile_n);
+// for the U-Net a batch class — 128 samples (the benchmark's CFG batch) for every batch of >= 64, so
+// a config-3 shard of 64 samples per rank (128 with CFG) and the whole 128-sample batch (256) sum
+// every output in the same order (bit-identical latents, test_gpu_multi.py); below 64 the batch itself
+// (each kernel's partial-tile rules keep a small batch and its shards alike: test_gpu_poison.py).
+static int dec_n(const Run& R, int N) { return R.tile_n > 0 ? R.tile_n : N >= 64 ? 128 : N; }
+
 // Output-channel tile of the halo-staged 3x3 conv for this GEMM, or 0 when it does not apply
 // (igemm_halo.h: 256-pixel tiles of whole rows of one sample, W = 16 / 32, 32-channel chunks,
 // >= 256 blocks without split-K, EPI_STATS).
 static int halo_bn(const Run& R, int src_C, int N, int H, int W, const ConvW& cw, int epi, bool plain_or_planes) {
-  const int Md = (R.tile_n > 0 ? R.tile_n : N) * H * W;
+  const int Md = dec_n(R, N) * H * W;
   const bool x3 = R.m->prec >= 1 && cw.Bh != nullptr;
   if (!(halo_enabled() && x3 && epi == EPI_STATS && cw.phases == 1 && cw.taps == 9 && (W == 16 || W == 32) &&
         (H * W) % 256 == 0 && src_C % 32 == 0 && cw.kpad == 9 * src_C && cw.Fh != nullptr && plain_or_planes))
@@ -871,6 +878,17 @@ static int halo_ms_mode() {
   return v;
 }
 static bool halo_ms_enabled() { return halo_ms_mode() != 0; }
+
+// GELU form of the exact-fp32 mode (training forward, fp32 reference mode): the erf form, as the
+// reference.  DMX_EXACT_GELU=fit (VERDICT r3 item 7 study, tools/gelu_train_study.py) runs the
+// inference fit there too.
+static int gelu_exact_flag(const Run& R) {
+  static const bool fit = [] {
+    const char* e = std::getenv("DMX_EXACT_GELU");
+    return e != nullptr && std::string(e) == "fit";
+  }();
+  return R.m->prec == 0 && !fit ? 1 : 0;
+}
 
 // DMX_WINO (same-box A/B): 1 (default) the halo convs at 16x16 / 32x32 run as Winograd F(2x2, 3x3)
 // (igemm_wino.h) in the x3 mode; 0 keeps the direct halo kernels.
@@ -917,11 +935,13 @@ static int wino_plan(const Run& R, int src_C, int N, int H, int W, const ConvW& 
   if (!((W == 32 && H % 8 == 0) || (W == 16 && H == 16) || (W == 8 && H == 8))) return 0;
   if (!((wino_mask() >> (W == 8 ? 0 : W == 16 ? 1 : 2)) & 1)) return 0;
   if (src_C % 16 != 0 || cw.cout % 64 != 0 || (size_t)16 * cw.cout * src_C * 2 >= ((size_t)1 << 31)) return 0;
-  const int nref = (R.tile_n > 0 ? R.tile_n : N) >= 64 ? 128 : 2;
+  const int nref = dec_n(R, N) >= 64 ? 128 : 2;
   const int blocks = cdiv(nref * H * W, 256) * (cw.cout / 64), nch = src_C / 16;
   int sp = 1, cp = nch;
   if (blocks < 256) {
-    if (!wino_split_enabled()) return 0;
+    // (small-batch class: the split Winograd conv lost to the direct kernels — config 5, B = 1 CFG:
+    // 1.44 vs 1.31 ms per step, same box)
+    if (!wino_split_enabled() || nref < 128) return 0;
     sp = std::max(1, std::min(nch, cdiv(256, blocks)));
     cp = cdiv(nch, sp);
     sp = cdiv(nch, cp);
@@ -932,13 +952,19 @@ static int wino_plan(const Run& R, int src_C, int N, int H, int W, const ConvW& 
 static bool wino_any(const Run& R, int src_C, int N, int H, int W, const ConvW& cw) {
   return wino_plan(R, src_C, N, H, W, cw, nullptr) > 0;
 }
+// GroupNorm(-residual)-GELU on load into a Winograd conv is applied once per 64-channel output block,
+// i.e. Cout / 64 times per staged element, on the VALU the input transform already loads (diagnostic
+// build without it: -11 % per step).  Same-box per-conv A/B against a norm_kernel pass + plain
+// staging: Cout = 64 GN + GELU fused wins (-8 us at 32x32, -6 us at 16x16 split), Cout = 128 even,
+// Cout >= 256 and every GroupNorm-residual-GELU (which also reads the residual) lose 10-42 us.
+static bool wino_gna_pays(const ConvW& cw, int gna) { return gna == 1 && cw.cout <= 64; }
 
 // Low-resolution halo conv (igemm_halo.h, W = 8 / 4 square maps): 256-pixel tiles of whole samples,
 // K split over 32-channel chunks until the grid has >= 256 blocks.  Returns the output-channel tile
 // (0: not applicable) and the split count / chunks per split.
 static int halo_ms_bn(const Run& R, int src_C, int N, int H, int W, const ConvW& cw, int epi, bool plain_or_planes,
                       int* splits, int* cps) {
-  const int Md = (R.tile_n > 0 ? R.tile_n : N) * H * W;
+  const int Md = dec_n(R, N) * H * W;
   const bool x3 = R.m->prec >= 1 && cw.Bh != nullptr;
   if (!(halo_ms_enabled() && x3 && epi == EPI_STATS && cw.phases == 1 && cw.taps == 9 && H == W &&
         (W == 8 || W == 4) && src_C % 32 == 0 &&
@@ -975,7 +1001,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
                 const float* res, float2* rowpart, int seg, const _Float16* ash = nullptr,
                 const _Float16* asl = nullptr, Deferred* defer = nullptr, const GnLoad* gn = nullptr) {
   const int M = N * H * W;
-  const int Md = (R.tile_n > 0 ? R.tile_n : N) * H * W;  // rows the decisions below are taken for
+  const int Md = dec_n(R, N) * H * W;  // rows the decisions below are taken for
   if (cw.cout % 32 != 0) throw Error(DMX_E_INTERNAL, "gemm: Cout must be a multiple of 32");
   if (src_mode == SRC_NCHW && epi == EPI_STATS && cw.taps == 9 && cw.phases == 1 && cw.cin == 4 && cw.cout == 64 &&
       W % 32 == 0 && seg == 32 && cw.bias == nullptr && R.m->kind != DMX_VAE && gn == nullptr) {
@@ -1073,7 +1099,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   p.partial = partial;
   p.rgrp = rgrp;
   p.nphase = cw.phases;
-  p.gexact = R.m->prec == 0 ? 1 : 0;
+  p.gexact = gelu_exact_flag(R);
   if (s.C != cw.cin) throw Error(DMX_E_INTERNAL, "gemm: source channels != weight channels");
   if (x3 && cw.cin < bk) throw Error(DMX_E_INTERNAL, "gemm: x3 path needs Cin >= K-step");
   if (ash != nullptr && !x3) throw Error(DMX_E_INTERNAL, "gemm: f16-plane operand needs the split GEMM");
@@ -1137,7 +1163,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
     R.end();
     HIPCHK(hipGetLastError());
     if (splits == 1 || (defer != nullptr && defer->fused)) return rrows;
-    SplitkParams q{partial, splits, M, cw.cout, cw.bias, res, out, rowpart, seg, epi, R.m->prec == 0 ? 1 : 0};
+    SplitkParams q{partial, splits, M, cw.cout, cw.bias, res, out, rowpart, seg, epi, gelu_exact_flag(R)};
     const int rb = cdiv(M * (cw.cout / 4), 256);
     R.begin("splitk_reduce_kernel", 0.0, 4.0 * (double)(splits + 1) * M * cw.cout);
     splitk_reduce_kernel<<<rb, 256, 0, R.st>>>(q);
@@ -1155,7 +1181,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
     R.end();
     HIPCHK(hipGetLastError());
     if (defer != nullptr && defer->fused) return rrows;  // the caller's reduce_norm_kernel sums the slabs
-    SplitkParams q{partial, splits, M, cw.cout, cw.bias, res, out, rowpart, seg, epi, R.m->prec == 0 ? 1 : 0};
+    SplitkParams q{partial, splits, M, cw.cout, cw.bias, res, out, rowpart, seg, epi, gelu_exact_flag(R)};
     const int rb = cdiv(M * (cw.cout / 4), 256);
     R.begin("splitk_reduce_kernel", 0.0, 4.0 * (double)(splits + 1) * M * cw.cout);
     splitk_reduce_kernel<<<rb, 256, 0, R.st>>>(q);
@@ -1186,7 +1212,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
       R.end();
       HIPCHK(hipGetLastError());
       if (splits == 1 || (defer != nullptr && defer->fused)) return rrows;
-      SplitkParams q{partial, splits, M, cw.cout, cw.bias, res, out, rowpart, seg, epi, R.m->prec == 0 ? 1 : 0};
+      SplitkParams q{partial, splits, M, cw.cout, cw.bias, res, out, rowpart, seg, epi, gelu_exact_flag(R)};
       R.begin("splitk_reduce_kernel", 0.0, 4.0 * (double)(splits + 1) * M * cw.cout);
       splitk_reduce_kernel<<<cdiv(M * (cw.cout / 4), 256), 256, 0, R.st>>>(q);
       R.end();
@@ -1241,7 +1267,7 @@ static void gn_finalize(Run& R, const float2* rowpart, float2* stats, int N, int
 // or precomputed (stats).
 static void norm(Run& R, NormParams np, int N) {
   if (R.plan) return;
-  np.gexact = R.m->prec == 0 ? 1 : 0;
+  np.gexact = gelu_exact_flag(R);
   // ~2048+ blocks in total, 256..1024 float4 per block (chunks are rounded up to 256 in-kernel)
   const int per = np.HW * (np.C / 4);
   const int target = 1024;  // total blocks aimed at for small tensors (measured +0.3 % over 2048)
@@ -1256,7 +1282,7 @@ static void norm(Run& R, NormParams np, int N) {
 // block per source sample; np describes the normalisation exactly as for norm().
 static void reduce_norm(Run& R, const Deferred& d, NormParams np, int n_src_samples) {
   if (R.plan) return;
-  np.gexact = R.m->prec == 0 ? 1 : 0;
+  np.gexact = gelu_exact_flag(R);
   const int kv = cdiv(np.HW * (np.C / 4), 1024);
   const int n_out = np.n_src > 0 ? 2 * n_src_samples : n_src_samples;
   const int kvt = kv <= 1 ? 1 : kv <= 2 ? 2 : kv <= 4 ? 4 : RN_MAXV;
@@ -1356,7 +1382,8 @@ static float* resblock(Run& R, const ResW& w, const SrcDesc& in, int mode, int N
   // the halo conv and conv1 wrote whole-sample partials (no split-K slabs): no norm_kernel launch,
   // no hi / lo planes.  DMX_GN_FUSE=0 turns it off (the staged operand is the same either way).
   const bool fuse1 = gn_fuse_enabled() && !d1.fused && !R.m->debug &&
-                     ((planes && halo_bn(R, w.mid, N, H, W, w.c2, EPI_STATS, true) > 0) || c2_wino);
+                     ((planes && halo_bn(R, w.mid, N, H, W, w.c2, EPI_STATS, true) > 0) ||
+                      (c2_wino && wino_gna_pays(w.c2, 1)));
   int rr2;
   if (fuse1) {
     GnLoad g;
@@ -1716,7 +1743,8 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
     GnLoad dly;
     const bool r1_wino = wino_any(R, u.C, N, sh[si], sw[si], m->up[i].r1.c1);
     const bool try_defer = gn_fuse_enabled() && !R.m->debug && R.m->prec >= 1 &&
-                           (halo_bn(R, u.C, N, sh[si], sw[si], m->up[i].r1.c1, EPI_STATS, true) > 0 || r1_wino);
+                           (r1_wino ? wino_gna_pays(m->up[i].r1.c1, 2)
+                                    : halo_bn(R, u.C, N, sh[si], sw[si], m->up[i].r1.c1, EPI_STATS, true) > 0);
     float* h0 = resblock(R, m->up[i].r0, plain_src(cat, u.C), SRC_PLAIN, N, sh[si], sw[si], true, nullptr, 0, 0, 0,
                          cat_h, cat_l, m->up[i].r1.c1.Bh != nullptr && !r1_wino, &hp, try_defer ? &dly : nullptr);
     R.layer = "up" + std::to_string(i + 1) + ".1";

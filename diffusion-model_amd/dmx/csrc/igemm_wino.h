@@ -41,6 +41,13 @@
 
 namespace dmx {
 
+// Diagnostic builds only (-DDMX_WDIAG=bits; wrong results, timing decomposition): 1 no MFMAs,
+// 2 no A-fragment arithmetic (LDS reads kept), 4 no GroupNorm / GELU in the halo store, 8 no output
+// stores.
+#ifndef DMX_WDIAG
+#define DMX_WDIAG 0
+#endif
+
 // U = G g Gᵀ of one 3x3 kernel for position (i, j), in double (exact products of ½-multiples).
 DMX_DEV double wino_u(const double (&g)[3][3], int i, int j) {
   double r[3];  // (G g)[i][b]
@@ -205,7 +212,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
 #pragma unroll
     for (int k = 0; k < NPI; ++k) {
       floatx4 v = ha[k];
-      if constexpr (GNA) {  // GroupNorm (+ residual) + GELU of the raw source; zero padding stays zero
+      if constexpr (GNA && !(DMX_WDIAG & 4)) {  // GroupNorm (+ residual) + GELU of the raw source; zero padding stays zero
         const float2 gst = gst_s[SPB == 1 ? 0 : min(((tid + 512 * k) >> 2) / HC / PS, SPB - 1)];
         v = gn_apply4v(v, gst, ggam, gbet, GNA == 1 ? 1 : 0);
         if constexpr (GNA == 2) {
@@ -265,8 +272,23 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
       for (int k = 0; k < 3; ++k) {
         const floatx4 da = *reinterpret_cast<const floatx4*>(hb + oa + oc[k] + 4 * h);
         const floatx4 db = *reinterpret_cast<const floatx4*>(hb + ob + oc[k] + 4 * h);
+        if constexpr (DMX_WDIAG & 2) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) T[k][e] = k == 2 ? db[e] : da[e];
+          continue;
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) T[k][e] = fmaf(db[e], sr, da[e]);
+      }
+      if constexpr (DMX_WDIAG & 2) {
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          vh[0][2 * h + e / 2] = __builtin_bit_cast(unsigned, T[0][e]) & 0x3bff3bffu;  // (finite f16)
+          vl[0][2 * h + e / 2] = __builtin_bit_cast(unsigned, T[1][e + 1]) & 0x3bff3bffu;
+          vh[1][2 * h + e / 2] = __builtin_bit_cast(unsigned, T[2][e]) & 0x3bff3bffu;
+          vl[1][2 * h + e / 2] = __builtin_bit_cast(unsigned, T[1][e]) & 0x3bff3bffu;
+        }
+        continue;
       }
 #pragma unroll
       for (int e = 0; e < 4; e += 2) {
@@ -322,9 +344,13 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
     for (int q = 0; q < 2; ++q)
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
-        acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[q], bh[q][n], acc[q][i][n], 0, 0, 0);
-        acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[q], bl[q][n], acc[q][i][n], 0, 0, 0);
-        acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[q], bh[q][n], acc[q][i][n], 0, 0, 0);
+        if constexpr (DMX_WDIAG & 1) {
+          asm volatile("" ::"v"(al[q]), "v"(ah[q]), "v"(bh[q][n]), "v"(bl[q][n]));
+        } else {
+          acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[q], bh[q][n], acc[q][i][n], 0, 0, 0);
+          acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[q], bl[q][n], acc[q][i][n], 0, 0, 0);
+          acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[q], bh[q][n], acc[q][i][n], 0, 0, 0);
+        }
         if (reload) {
           load_b(q, n, -1);
           __builtin_amdgcn_sched_barrier(0x0086);
@@ -404,7 +430,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
           for (int s = 0; s < 2; ++s) {
             const float y = (r == 0 ? (z[0][s] + z[1][s]) + z[2][s] : (z[1][s] - z[2][s]) - z[3][s]) + bias;
             const int oy = y0 + 2 * ty + r, ox = 2 * tx + s;
-            if (nsmp + st < nsamp) dst[(((size_t)(nsmp + st) * p.H + oy) * W + ox) * p.Cout + col] = y;
+            if (!(DMX_WDIAG & 8) && nsmp + st < nsamp) dst[(((size_t)(nsmp + st) * p.H + oy) * W + ox) * p.Cout + col] = y;
             s1 += y;
             s2 += y * y;
           }
