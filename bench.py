@@ -299,8 +299,11 @@ def train_leg(args, dev, world=1, rank=0):
 
 MFMA_FAMILIES = ("igemm_x3_kernel", "igemm_pp_kernel", "igemm_f32_kernel", "attention_x3_kernel",
                  "attention16_kernel", "attention_kernel", "tok_ln_qkv_kernel", "tok_ln_qkv_lds_kernel",
-                 "tok_attn_out_kernel", "igemm_halo_kernel", "igemm_halo_cs_kernel")
-X3_FAMILIES = ("igemm_pp_kernel", "attention16_kernel", "igemm_halo_kernel", "igemm_halo_cs_kernel")
+                 "tok_attn_out_kernel", "igemm_halo_kernel", "igemm_halo_cs_kernel", "wino_kernel")
+X3_FAMILIES = ("igemm_pp_kernel", "attention16_kernel", "igemm_halo_kernel", "igemm_halo_cs_kernel", "wino_kernel")
+# Winograd F(2x2, 3x3): the algorithmic work is the reference's direct conv (2 M Cout 9 Cin); the
+# kernel issues 16 / 36 of those multiply-adds on the matrix cores
+WINO_EXECUTED = 16.0 / 36.0
 
 
 def family(name):
@@ -321,6 +324,9 @@ def _entry(fam, a, pmc_fam):
         e = {"kernel": fam, "bound": "mfma", "mfma_dtype": mfma, "achieved": round(achieved, 3),
              "peak": round(peak, 1), "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
              "flops_per_launch": per_launch}
+        if fam == "wino_kernel":
+            e["work"] = "direct-conv FLOPs (reference work); executed MFMA work = 16/36 of it"
+            e["executed_frac_of_peak"] = round(achieved * WINO_EXECUTED / peak, 4)
     else:
         per_launch = a["bytes"] / a["n"]
         achieved = per_launch / (avg_ms * 1e-3) / 1e9

@@ -704,6 +704,35 @@ struct Prof {
   }
 };
 
+// DMX_CKSUM=1 (diagnostic, eager dmx_step / dmx_unet_forward only): the workspace is filled with
+// 0xFF before the step and, after every kernel, the 64-bit sum of its used part is recorded; at the
+// end of the step the sums are compared with the previous step's and the first kernel after which
+// they differ is printed (a race localiser: identical inputs must give identical sums).
+static bool cksum_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("DMX_CKSUM");
+    return e != nullptr && std::atoi(e) != 0;
+  }();
+  return v;
+}
+static __global__ void cksum_kernel(const unsigned* p, size_t n, unsigned long long* slot) {
+  unsigned long long s = 0;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) s += p[i] * (i | 1);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(slot, s);
+}
+struct Cksum {
+  unsigned long long* dev = nullptr;
+  std::vector<std::string> names, prev_names;
+  std::vector<unsigned long long> prev;
+  int runs = 0;
+};
+static Cksum& cksum_state() {
+  static Cksum c;
+  return c;
+}
+
 struct Run {
   dmx_model* m;
   hipStream_t st;
@@ -717,13 +746,22 @@ struct Run {
   // function of the per-sample geometry only).
   int tile_n = 0;
   void tap(const std::string& name, const float* p, size_t count);
+  std::string last;
   void begin(const std::string& kernel, double flops, double bytes) {
+    if (cksum_enabled()) last = layer + " " + kernel;
     if (!prof) return;
     ProfRec r{kernel, layer, flops, bytes, prof->ev(), prof->ev()};
     HIPCHK(hipEventRecord(r.e0, st));
     prof->recs.push_back(r);
   }
   void end() {
+    if (cksum_enabled() && !plan && m->ws_mem != nullptr) {
+      Cksum& c = cksum_state();
+      if (c.names.size() < 1024) {
+        cksum_kernel<<<1024, 256, 0, st>>>(static_cast<const unsigned*>(m->ws_mem), ws.off / 4, c.dev + c.names.size());
+        c.names.push_back(last);
+      }
+    }
     if (!prof) return;
     HIPCHK(hipEventRecord(prof->recs.back().e1, st));
   }
@@ -1835,9 +1873,32 @@ static void run_planned(dmx_model* m, hipStream_t st, F&& body) {
   m->ws.base = static_cast<char*>(m->ws_mem);
   m->ws.off = 0;
   m->ws.plan = false;
+  Cksum& ck = cksum_state();
+  if (cksum_enabled()) {
+    if (ck.dev == nullptr) HIPCHK(hipMalloc(&ck.dev, 1024 * sizeof(unsigned long long)));
+    HIPCHK(hipMemsetAsync(ck.dev, 0, 1024 * sizeof(unsigned long long), st));
+    HIPCHK(hipMemsetAsync(m->ws_mem, 0xFF, planned, st));
+    ck.names.clear();
+  }
   Run R{m, st, false, m->ws};
   body(R);
   if (m->ws.off != planned) throw Error(DMX_E_INTERNAL, "workspace plan / run mismatch");
+  if (cksum_enabled()) {
+    std::vector<unsigned long long> h(ck.names.size());
+    HIPCHK(hipMemcpyAsync(h.data(), ck.dev, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (ck.names == ck.prev_names) {
+      for (size_t k = 0; k < h.size(); ++k)
+        if (h[k] != ck.prev[k]) {
+          std::fprintf(stderr, "[dmx cksum] run %d: first difference after kernel %zu (%s)\n", ck.runs, k,
+                       ck.names[k].c_str());
+          break;
+        }
+    }
+    ck.prev = h;
+    ck.prev_names = ck.names;
+    ++ck.runs;
+  }
 }
 
 // t_next (multi-step sample-loop graphs): the step's t - 1 is stored there by the embedding kernel.

@@ -33,5 +33,5 @@ for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
   timeout -k 10 300 rocprofv3 --pmc $set -d gpurun_out/pmc_sq$i -o run --output-format csv -- python3 bench.py $PMC_ARGS > gpurun_out/pmc_sq$i.log 2>&1
   i=$((i+1))
 done
-python3 tools/pmc_sq.py "igemm|attention|norm|tok_|prep|step_tail|embed" > $OUT/${TAG}_sq_counters.txt
+python3 tools/pmc_sq.py "igemm|wino|conv_in|attention|norm|tok_|prep|step_tail|embed" > $OUT/${TAG}_sq_counters.txt
 echo "[profile] sq ok"
