@@ -705,9 +705,10 @@ struct Prof {
 };
 
 // DMX_CKSUM=1 (diagnostic, eager dmx_step / dmx_unet_forward only): the workspace is filled with
-// 0xFF before the step and, after every kernel, the 64-bit sum of its used part is recorded; at the
-// end of the step the sums are compared with the previous step's and the first kernel after which
-// they differ is printed (a race localiser: identical inputs must give identical sums).
+// 0xFF before the step and, at the end of every layer, a 64-bit weighted sum of its used part is
+// recorded; at the end of the step the sums are compared with the previous step's and the first
+// layer after which they differ is printed (a race localiser: identical inputs must give identical
+// sums).
 static bool cksum_enabled() {
   static const bool v = [] {
     const char* e = std::getenv("DMX_CKSUM");
@@ -746,22 +747,25 @@ struct Run {
   // function of the per-sample geometry only).
   int tile_n = 0;
   void tap(const std::string& name, const float* p, size_t count);
-  std::string last;
+  std::string ck_layer;
+  // DMX_CKSUM: one workspace checksum per layer, taken when the next layer's first kernel begins
+  void ck() {
+    Cksum& c = cksum_state();
+    if (plan || m->ws_mem == nullptr || ck_layer.empty() || c.names.size() >= 1024) return;
+    cksum_kernel<<<1024, 256, 0, st>>>(static_cast<const unsigned*>(m->ws_mem), ws.off / 4, c.dev + c.names.size());
+    c.names.push_back(ck_layer);
+  }
   void begin(const std::string& kernel, double flops, double bytes) {
-    if (cksum_enabled()) last = layer + " " + kernel;
+    if (cksum_enabled() && layer != ck_layer) {
+      ck();
+      ck_layer = layer;
+    }
     if (!prof) return;
     ProfRec r{kernel, layer, flops, bytes, prof->ev(), prof->ev()};
     HIPCHK(hipEventRecord(r.e0, st));
     prof->recs.push_back(r);
   }
   void end() {
-    if (cksum_enabled() && !plan && m->ws_mem != nullptr) {
-      Cksum& c = cksum_state();
-      if (c.names.size() < 1024) {
-        cksum_kernel<<<1024, 256, 0, st>>>(static_cast<const unsigned*>(m->ws_mem), ws.off / 4, c.dev + c.names.size());
-        c.names.push_back(last);
-      }
-    }
     if (!prof) return;
     HIPCHK(hipEventRecord(prof->recs.back().e1, st));
   }
@@ -817,6 +821,28 @@ static int split_below() {
   static const int v = [] {
     const char* e = std::getenv("DMX_SPLIT_BELOW");
     return e == nullptr ? 256 : std::atoi(e);
+  }();
+  return v;
+}
+// Smallest reduce_norm_kernel instance used (DMX_RN_MINKV, default 2).  The one-float4-per-thread
+// instance (KV = 1: the 4x4 C = 256 ResBlocks) gave run-to-run different outputs when a second
+// process shared the GPU (tools/conc_step.sh + DMX_CKSUM per-layer workspace checksums: the first
+// difference always after down3.0 / down3.1 / bot3, the three layers that use it; 9 of 9 runs in
+// one arm), while the KV = 2 instance on the same data — and splitk_reduce + norm_kernel — never
+// did (0 of 72).  No LDS or global hazard was found in its code; until the cause is known it is
+// not used.
+static int rn_minkv() {
+  static const int v = [] {
+    const char* e = std::getenv("DMX_RN_MINKV");
+    return e == nullptr ? 2 : std::atoi(e);
+  }();
+  return v;
+}
+// DMX_RN_FUSE (race bisection): 0 = split-K slabs reduced by splitk_reduce_kernel + norm_kernel
+static bool rn_fuse_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("DMX_RN_FUSE");
+    return e == nullptr || std::atoi(e) != 0;
   }();
   return v;
 }
@@ -1103,7 +1129,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   const int rgrp = (splits == 1 && (H * W) % 32 == 0) ? 32 : 1;
   const int rrows = (wino && splits == 1) ? H * W / 16 : cw.phases * H * W / rgrp;  // GroupNorm partial rows / sample
   if (defer != nullptr) {
-    defer->fused = splits > 1 && epi == EPI_STATS && !R.m->debug &&
+    defer->fused = splits > 1 && epi == EPI_STATS && !R.m->debug && rn_fuse_enabled() &&
                    H * W * (cw.cout / 4) <= RN_MAXV * 1024;  // (debug taps read the raw conv output)
     defer->partial = partial;
     defer->splits = splits;
@@ -1321,7 +1347,7 @@ static void norm(Run& R, NormParams np, int N) {
 static void reduce_norm(Run& R, const Deferred& d, NormParams np, int n_src_samples) {
   if (R.plan) return;
   np.gexact = gelu_exact_flag(R);
-  const int kv = cdiv(np.HW * (np.C / 4), 1024);
+  const int kv = std::max(rn_minkv(), cdiv(np.HW * (np.C / 4), 1024));
   const int n_out = np.n_src > 0 ? 2 * n_src_samples : n_src_samples;
   const int kvt = kv <= 1 ? 1 : kv <= 2 ? 2 : kv <= 4 ? 4 : RN_MAXV;
   R.begin("reduce_norm_kernel<" + std::to_string(kvt) + ">", 0.0,
@@ -1884,6 +1910,7 @@ static void run_planned(dmx_model* m, hipStream_t st, F&& body) {
   body(R);
   if (m->ws.off != planned) throw Error(DMX_E_INTERNAL, "workspace plan / run mismatch");
   if (cksum_enabled()) {
+    R.ck();
     std::vector<unsigned long long> h(ck.names.size());
     HIPCHK(hipMemcpyAsync(h.data(), ck.dev, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));

@@ -12,7 +12,7 @@ for v in "$@"; do
   wait $pa
   ra=$?
   echo "== $v"
-  grep -ah "runs" gpurun_out/sA.log gpurun_out/sB.log
+  grep -ah "runs\|cksum" gpurun_out/sA.log gpurun_out/sB.log
   [ $ra -ne 0 -o $rb -ne 0 ] && { echo "arm $v failed ($ra/$rb)"; tail -3 gpurun_out/sA.log gpurun_out/sB.log; exit 1; }
 done
 exit 0
