@@ -43,9 +43,17 @@ namespace dmx {
 
 // Diagnostic builds only (-DDMX_WDIAG=bits; wrong results, timing decomposition): 1 no MFMAs,
 // 2 no A-fragment arithmetic (LDS reads kept), 4 no GroupNorm / GELU in the halo store, 8 no output
-// stores.
+// stores, 16 the output bytes stored as two contiguous float4 per thread (wrong layout).
 #ifndef DMX_WDIAG
 #define DMX_WDIAG 0
+#endif
+
+// Output stores carry the non-temporal hint (DMX_WNT=0 builds plain stores for A/B): the output is
+// streamed to memory instead of sitting dirty in the XCDs' L2s until the end-of-kernel writeback —
+// every Winograd launch 1.4-7 us faster, its consumers (norm / reduce_norm, now reading it from
+// memory) 0.1-1.7 us slower: +1.5-1.7 % per CFG step, 3 / 3 same-box rounds.
+#ifndef DMX_WNT
+#define DMX_WNT 1
 #endif
 
 // U = G g Gᵀ of one 3x3 kernel for position (i, j), in double (exact products of ½-multiples).
@@ -415,6 +423,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
       const float bias = (EPI == EPI_STATS && p.bias != nullptr) ? p.bias[col] : 0.f;
       float* dst = EPI == EPI_PARTIAL ? p.partial + (size_t)bz * p.M * p.Cout : p.out;
       float s1 = 0.f, s2 = 0.f;
+      float ys[8];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         float z[4][2];
@@ -430,10 +439,23 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
           for (int s = 0; s < 2; ++s) {
             const float y = (r == 0 ? (z[0][s] + z[1][s]) + z[2][s] : (z[1][s] - z[2][s]) - z[3][s]) + bias;
             const int oy = y0 + 2 * ty + r, ox = 2 * tx + s;
-            if (!(DMX_WDIAG & 8) && nsmp + st < nsamp) dst[(((size_t)(nsmp + st) * p.H + oy) * W + ox) * p.Cout + col] = y;
+            if (!(DMX_WDIAG & 24) && nsmp + st < nsamp) {
+              float* a = &dst[(((size_t)(nsmp + st) * p.H + oy) * W + ox) * p.Cout + col];
+              if constexpr (DMX_WNT) __builtin_nontemporal_store(y, a);
+              else *a = y;
+            }
+            ys[4 * e + 2 * r + s] = y;
             s1 += y;
             s2 += y * y;
           }
+      }
+      if constexpr ((DMX_WDIAG & 16) != 0) {  // same bytes as two contiguous float4 per thread (wrong layout)
+        const size_t blin = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+        if ((blin + 1) * 16384 <= (size_t)p.M * p.Cout) {
+          float* q = dst + blin * 16384 + (2 * mb + n) * 4096 + tid * 8;
+          *reinterpret_cast<floatx4*>(q) = floatx4{ys[0], ys[1], ys[2], ys[3]};
+          *reinterpret_cast<floatx4*>(q + 4) = floatx4{ys[4], ys[5], ys[6], ys[7]};
+        }
       }
       // partial of 4 tiles (16 pixels) x 32 channels = this wave's 64 lanes
       if constexpr (EPI == EPI_STATS) {

@@ -68,6 +68,15 @@ DMX_DEV floatx4 bload_f4(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 
+// DMX_NT_ATT (A/B build): attention outputs stored with the non-temporal hint
+#ifndef DMX_NT_ATT
+#define DMX_NT_ATT 0
+#endif
+DMX_DEV void att_st4(float* a, floatx4 v) {
+  if constexpr (DMX_NT_ATT) __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(a));
+  else *reinterpret_cast<floatx4*>(a) = v;
+}
+
 // hi/lo split of two fp32 values as packed f16 pairs (common.h split2u: 3 VALU ops per pair).
 DMX_DEV void split2(f32x2 v, unsigned& h, unsigned& l) { split2u(v.x, v.y, h, l); }
 
@@ -585,7 +594,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
           floatx4 v;
 #pragma unroll
           for (int j = 0; j < 4; ++j) v[j] = o[dt][4 * g + j] * inv;
-          *reinterpret_cast<floatx4*>(out + ((size_t)n * L + q) * C + hd * D + d) = v;
+          att_st4(out + ((size_t)n * L + q) * C + hd * D + d, v);
         }
       }
   }
@@ -810,7 +819,7 @@ __global__ __launch_bounds__(NW * 64) void attention16_kernel(const float* qkv, 
         floatx4 v;
 #pragma unroll
         for (int j = 0; j < 4; ++j) v[j] = o[4 * g + j] * inv;
-        *reinterpret_cast<floatx4*>(out + ((size_t)n * L + q) * C + hd * D + d) = v;
+        att_st4(out + ((size_t)n * L + q) * C + hd * D + d, v);
       }
     }
   }

@@ -130,9 +130,9 @@ static __global__ __launch_bounds__(256) void embed_kernel(const EmbedParams p) 
 // inc's first conv (models/unet_cond.py:17, Conv2d(in_ch, 64, 3, padding=1, bias=False)) on the NCHW
 // network input: K = 9 taps x <= 4 channels is far too thin for a GEMM (the implicit GEMM padded it
 // to 64 and paid a global round trip per 16-deep K step), so it runs as a direct fp32 conv: a block
-// owns 32 output pixels (one image row, W % 32 == 0) x 64 channels, thread (pixel, 8-channel group)
-// accumulates its 36 products per channel in fixed (tap, channel) order with fp32 FMAs (exact fp32
-// semantics in every precision mode), the 64 x 36 weights staged in LDS.  Output NHWC fp32 plus the
+// owns 32 output pixels (one image row segment, W % 32 == 0) x 64 channels, each output accumulates
+// its 36 products in fixed (tap, channel) order with fp32 FMAs (exact fp32
+// semantics in every precision mode).  Output NHWC fp32 plus the
 // GroupNorm (sum, sum of squares) partial of each (32 pixels, 32 channels) group — the layout
 // igemm_epilogue writes (rgrp = 32, seg = 32).
 // ---------------------------------------------------------------------------
@@ -147,57 +147,60 @@ struct ConvInParams {
   int H, W;
 };
 static __global__ __launch_bounds__(256) void conv_in_kernel(const ConvInParams p) {
+  // thread (output channel co, pixel group pg): pixels 8 pg .. 8 pg + 7 of the block's 32; its 36
+  // weights in registers, the 3 x 34 x 4 input patch in LDS (float4 per pixel: one broadcast
+  // ds_read_b128 per pixel and tap), one coalesced 256-byte row of channels per pixel store
   __shared__ float ws[64][37];
-  __shared__ float2 red[4];
-  const int tid = threadIdx.x, px = tid & 31, g = tid >> 5;
+  __shared__ __attribute__((aligned(16))) float inl[3][34][4];
+  __shared__ float2 red[4][2];
+  const int tid = threadIdx.x, co = tid & 63, pg = tid >> 6;
   for (int i = tid; i < 64 * 36; i += 256) {
-    const int co = i / 36, k = i - co * 36, tap = k >> 2, c = k & 3;
-    ws[co][k] = c < p.cin ? p.B[(size_t)co * p.kpad + tap * p.cin + c] : 0.f;
+    const int o = i / 36, k = i - o * 36, tap = k >> 2, c = k & 3;
+    ws[o][k] = c < p.cin ? p.B[(size_t)o * p.kpad + tap * p.cin + c] : 0.f;
   }
   const int HW = p.H * p.W;
   const int m0 = blockIdx.x * 32;
-  const int n = m0 / HW, r = m0 - n * HW, y = r / p.W, x = r - y * p.W + px;
+  const int n = m0 / HW, r = m0 - n * HW, y = r / p.W, x0 = r - y * p.W;
   const int ns = p.n_mod ? n % p.n_mod : n;
-  float in[36];
-#pragma unroll
-  for (int tap = 0; tap < 9; ++tap) {
-    const int iy = y + tap / 3 - 1, ix = x + tap % 3 - 1;
-    const bool ok = iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const float v = (ok && c < p.creal) ? p.x[((size_t)ns * p.creal + c) * HW + (size_t)iy * p.W + ix] : 0.f;
-      in[tap * 4 + c] = p.scale != 1.f ? v / p.scale : v;
-    }
+  for (int i = tid; i < 3 * 34 * 4; i += 256) {
+    const int c = i / 102, rem = i - c * 102, ry = rem / 34, cx = rem - ry * 34;
+    const int iy = y + ry - 1, ix = x0 + cx - 1;
+    const bool ok = iy >= 0 && iy < p.H && ix >= 0 && ix < p.W && c < p.creal;
+    const float v = ok ? p.x[((size_t)ns * p.creal + c) * HW + (size_t)iy * p.W + ix] : 0.f;
+    inl[ry][cx][c] = p.scale != 1.f ? v / p.scale : v;
   }
   __syncthreads();
-  float acc[8];
+  float w[36];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float a = 0.f;
-#pragma unroll
-    for (int k = 0; k < 36; ++k) a = fmaf(ws[8 * g + j][k], in[k], a);
-    acc[j] = a;
-  }
-  float* o = p.out + ((size_t)m0 + px) * 64 + 8 * g;
-  *reinterpret_cast<floatx4*>(o) = floatx4{acc[0], acc[1], acc[2], acc[3]};
-  *reinterpret_cast<floatx4*>(o + 4) = floatx4{acc[4], acc[5], acc[6], acc[7]};
-  // GroupNorm partials: segment s = channels 32 s .. + 31 = groups g in [4 s, 4 s + 3] = waves 2 s, 2 s + 1
+  for (int k = 0; k < 36; ++k) w[k] = ws[co][k];
+  float* o = p.out + (size_t)m0 * 64 + co;
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    s1 += acc[j];
-    s2 += acc[j] * acc[j];
-  }
+    const int px = 8 * pg + j;
+    float a = 0.f;
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
+    for (int tap = 0; tap < 9; ++tap) {  // (tap, channel) order as the packed weights
+      const floatx4 v = *reinterpret_cast<const floatx4*>(&inl[tap / 3][px + tap % 3][0]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) a = fmaf(w[tap * 4 + c], v[c], a);
+    }
+    o[(size_t)px * 64] = a;
+    s1 += a;
+    s2 += a * a;
+  }
+  // GroupNorm partials: segment s = channels 32 s .. + 31 = lanes 32 s .. + 31 of every wave
+#pragma unroll
+  for (int off = 1; off < 32; off <<= 1) {
     s1 += __shfl_xor(s1, off, 64);
     s2 += __shfl_xor(s2, off, 64);
   }
-  if ((tid & 63) == 0) red[tid >> 6] = make_float2(s1, s2);
+  if ((tid & 31) == 0) red[pg][co >> 5] = make_float2(s1, s2);
   __syncthreads();
   if (tid < 2)
     p.rowpart[((size_t)n * (HW / 32) + r / 32) * 2 + tid] =
-        make_float2(red[2 * tid].x + red[2 * tid + 1].x, red[2 * tid].y + red[2 * tid + 1].y);
+        make_float2((red[0][tid].x + red[1][tid].x) + (red[2][tid].x + red[3][tid].x),
+                    (red[0][tid].y + red[1][tid].y) + (red[2][tid].y + red[3][tid].y));
 }
 
 // ---------------------------------------------------------------------------
@@ -263,6 +266,14 @@ struct NormParams {
   _Float16* out_h; _Float16* out_l;  // optional fp16 hi/lo planes (split-precision GEMM operand)
 };
 
+// DMX_NT_NORM (A/B build): norm_kernel / prep_kernel outputs stored with the non-temporal hint
+#ifndef DMX_NT_NORM
+#define DMX_NT_NORM 0
+#endif
+DMX_DEV void st4(float* a, floatx4 v) {
+  if constexpr (DMX_NT_NORM) __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(a));
+  else *reinterpret_cast<floatx4*>(a) = v;
+}
 static __global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
   const int n = blockIdx.y, tid = threadIdx.x;
   const int ns = p.n_src > 0 ? n % p.n_src : n;  // source sample (CFG-shared trunk prefix)
@@ -359,7 +370,7 @@ static __global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
         for (int j = 0; j < 4; ++j) o[j] += e[j];
       }
       const size_t off = base + (size_t)idx * 4;
-      if (p.out != nullptr) *reinterpret_cast<floatx4*>(p.out + off) = o;
+      if (p.out != nullptr) st4(p.out + off, o);
       if (p.out_h != nullptr) {
         half4 hh, ll;
         split4(o, hh, ll);
@@ -517,7 +528,7 @@ __global__ __launch_bounds__(256) void prep_kernel(const SrcDesc s, float* out, 
     const int rr = (int)(pix - (size_t)n * H * W);
     const int y = rr / W, x = rr - y * W;
     const floatx4 v = load_src4<SRC>(s, n, y, x, c, H, W);
-    *reinterpret_cast<floatx4*>(out + pix * s.C + c) = v;
+    st4(out + pix * s.C + c, v);
     if (oh != nullptr) {
       half4 hh, ll;
       split4(v, hh, ll);
