@@ -164,10 +164,12 @@ class ShardedCondSampler:
         (B, 8H, 8W, 3) uint8 images (decode and a VAE given) or the (B, C, H, W) latents,
         None on the other ranks.  Draw order per rank equals the single-process sampler's
         (optional encode draw, x_T, then the seed (device mode) or one global draw per step
-        (host mode)), so every sample sees the single-process draws: rank 0's result equals the
-        single-process result up to fp32 summation order — the U-Net's split-K / tile decisions
-        follow the shard's batch size (latents within rel-L2 1e-5 in the tests; the VAE decode is
-        batch-invariant by construction, ``Run::tile_n``).
+        (host mode)), so every sample sees the single-process draws.  The U-Net takes its split-K
+        / tile decisions for a batch class (engine.hip ``dec_n``: 128 samples for every CFG batch
+        of >= 64, the batch itself below) and the VAE decode per sample (``Run::tile_n``), so
+        shards of >= 64 samples (config 3: 64 per rank) give rank 0 exactly the single-process
+        bytes (test_gpu_multi.py, bit-equal); smaller shards equal it up to fp32 summation order
+        (latents within rel-L2 1e-5 in the tests).
 
         The T loop runs in Diffuser.GUARD_CHUNK pieces with the single-process sampler's
         split-precision range guard: after each chunk every rank's range flag is OR-ed across
