@@ -43,7 +43,8 @@ namespace dmx {
 
 // Diagnostic builds only (-DDMX_WDIAG=bits; wrong results, timing decomposition): 1 no MFMAs,
 // 2 no A-fragment arithmetic (LDS reads kept), 4 no GroupNorm / GELU in the halo store, 8 no output
-// stores, 16 the output bytes stored as two contiguous float4 per thread (wrong layout).
+// stores, 16 the output bytes stored as two contiguous float4 per thread (wrong layout), 32 no LDS
+// round trip in the epilogue (outputs from the wave's own accumulators).
 #ifndef DMX_WDIAG
 #define DMX_WDIAG 0
 #endif
@@ -402,7 +403,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
     for (int n = 0; n < 2; ++n) {
       // positions -> LDS [xi][channel][tile] (rows of a lane's accumulator are 4 consecutive tiles)
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
+      for (int q = 0; q < ((DMX_WDIAG & 32) ? 0 : 2); ++q)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           floatx4 v;
@@ -414,6 +415,11 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
       float m[16][2];
 #pragma unroll
       for (int xi = 0; xi < 16; ++xi) {
+        if constexpr ((DMX_WDIAG & 32) != 0) {  // diagnostic: no LDS round trip (wrong values)
+          m[xi][0] = acc[xi & 1][mb][n][xi >> 1];
+          m[xi][1] = acc[(xi >> 1) & 1][mb][n][(xi + 3) & 15];
+          continue;
+        }
         const f32x2 v = *reinterpret_cast<const f32x2*>(&lds[(xi * 32 + cc) * EPP + 2 * tp]);
         m[xi][0] = v.x;
         m[xi][1] = v.y;
