@@ -914,7 +914,13 @@ struct GnLoad {
 // a config-3 shard of 64 samples per rank (128 with CFG) and the whole 128-sample batch (256) sum
 // every output in the same order (bit-identical latents, test_gpu_multi.py); below 64 the batch itself
 // (each kernel's partial-tile rules keep a small batch and its shards alike: test_gpu_poison.py).
-static int dec_n(const Run& R, int N) { return R.tile_n > 0 ? R.tile_n : N >= 64 ? 128 : N; }
+static int dec_n(const Run& R, int N) {
+  static const bool per_batch = [] {  // DMX_DEC_N=0 (A/B): decisions from the batch itself
+    const char* e = std::getenv("DMX_DEC_N");
+    return e != nullptr && std::atoi(e) == 0;
+  }();
+  return R.tile_n > 0 ? R.tile_n : (N >= 64 && !per_batch) ? 128 : N;
+}
 
 // Output-channel tile of the halo-staged 3x3 conv for this GEMM, or 0 when it does not apply
 // (igemm_halo.h: 256-pixel tiles of whole rows of one sample, W = 16 / 32, 32-channel chunks,
@@ -1665,6 +1671,8 @@ struct FwdIn {
   const int64_t* y; int y_null_first; int64_t y_null;
   const float* vals; const float* mask; int cond_rows;
   int64_t* t_next = nullptr;  // multi-step graphs: where the embedding kernel stores t - 1
+  bool cond_cached = false;   // multi-step graphs, steps after the first: the cond-MLP rows are
+                              // already in the workspace (t-independent, same address every step)
 };
 
 // UnetCond trunk (models/unet_cond_geom.py:52-76): returns the (N,H,W,64) feature
@@ -1703,10 +1711,12 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
     e.out = emb;
     R.layer = "embed";
     if (has_cond) {  // cond_mlp once per distinct condition row (the CFG halves share it)
-      R.begin("cond_emb_kernel", 2.0 * cond_rows * (24.0 * 256 + 256.0 * 256), 4.0 * (256.0 * 256 + 24.0 * 256));
-      cond_emb_kernel<<<cond_rows, 256, 0, R.st>>>(e, cnd);
-      R.end();
-      HIPCHK(hipGetLastError());
+      if (!in.cond_cached) {
+        R.begin("cond_emb_kernel", 2.0 * cond_rows * (24.0 * 256 + 256.0 * 256), 4.0 * (256.0 * 256 + 24.0 * 256));
+        cond_emb_kernel<<<cond_rows, 256, 0, R.st>>>(e, cnd);
+        R.end();
+        HIPCHK(hipGetLastError());
+      }
       e.cnd = cnd;
     }
     R.begin("embed_kernel", 2.0 * N * (24.0 * 256 + 256.0 * 256 + 256.0 * m->hsum), 4.0 * (256.0 * 256 + 256.0 * m->hsum));
@@ -1929,12 +1939,13 @@ static void run_planned(dmx_model* m, hipStream_t st, F&& body) {
 }
 
 // t_next (multi-step sample-loop graphs): the step's t - 1 is stored there by the embedding kernel.
-static void step_body(Run& R, const dmx_step_args& a, int64_t* t_next = nullptr) {
+static void step_body(Run& R, const dmx_step_args& a, int64_t* t_next = nullptr, bool cond_cached = false) {
   dmx_model* m = R.m;
   const bool cfg = m->kind != DMX_UNET && a.guidance > 0.f && a.y != nullptr;
   const int N = cfg ? 2 * a.n : a.n;
   FwdIn in{a.x_in, a.n, a.t, a.t_stride, a.y, cfg ? 1 : 0, a.null_label, a.vals, a.mask, a.n};
   in.t_next = t_next;
+  in.cond_cached = cond_cached;
   float* feat = unet_trunk(R, in, N, a.h, a.w);
   if (R.plan) return;
   StepTailParams p;
@@ -2456,7 +2467,7 @@ int dmx_sample_loop(dmx_model* m, const dmx_step_args* a, int steps, int use_gra
           Run R{m, st, false, m->ws};
           dmx_step_args ak = *a;
           ak.t = (k & 1) ? tscr : tdev;
-          step_body(R, ak, (k & 1) ? tdev : tscr);
+          step_body(R, ak, (k & 1) ? tdev : tscr, k > 0);  // cond MLP rows from step 0 of the graph
         }
       } catch (...) {
         hipGraph_t g;
