@@ -49,6 +49,10 @@ namespace dmx {
 #define DMX_WDIAG 0
 #endif
 
+#ifndef DMX_WEPP
+#define DMX_WEPP 36
+#endif
+
 // Output stores carry the non-temporal hint (DMX_WNT=0 builds plain stores for A/B): the output is
 // streamed to memory instead of sitting dirty in the XCDs' L2s until the end-of-kernel writeback —
 // every Winograd launch 1.4-7 us faster, its consumers (norm / reduce_norm, now reading it from
@@ -128,7 +132,10 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   constexpr int CK = 16;                    // channels per chunk
   constexpr int NPC = HR * HC * (CK / 4);   // float4 pieces per chunk
   constexpr int NPI = (NPC + 511) / 512;    // pieces per thread
-  constexpr int EPP = 36;                   // epilogue LDS row pitch (32 tiles + 4)
+  // epilogue LDS row pitch: 32 tiles + 2 — with 8-byte stores / reads, 34 cc mod 64 dwords puts
+  // the 32 lanes of each ds_read_b64 group on 32 distinct bank pairs (a pitch of 36, needed by
+  // 16-byte stores, made every read 2-way conflicted)
+  constexpr int EPP = DMX_WEPP;
   constexpr int EPF = 16 * 32 * EPP;        // epilogue floats (one 32 x 32 pass, 16 positions)
   constexpr int LDSF = 2 * HBUF + 1024 > EPF ? 2 * HBUF + 1024 : EPF;
   __shared__ __attribute__((aligned(16))) float lds[LDSF];
@@ -409,7 +416,13 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
           floatx4 v;
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = acc[q][mb][n][4 * k + e] * P.inv_scale;
-          *reinterpret_cast<floatx4*>(&lds[((xi0 + q) * 32 + fr) * EPP + 8 * k + 4 * fh]) = v;
+          float* e = &lds[((xi0 + q) * 32 + fr) * EPP + 8 * k + 4 * fh];
+          if constexpr (EPP % 4 == 0) {
+            *reinterpret_cast<floatx4*>(e) = v;
+          } else {
+            *reinterpret_cast<f32x2*>(e) = f32x2{v[0], v[1]};
+            *reinterpret_cast<f32x2*>(e + 2) = f32x2{v[2], v[3]};
+          }
         }
       __syncthreads();
       float m[16][2];
