@@ -50,7 +50,7 @@ namespace dmx {
 #endif
 
 #ifndef DMX_WEPP
-#define DMX_WEPP 36
+#define DMX_WEPP 34
 #endif
 
 // Output stores carry the non-temporal hint (DMX_WNT=0 builds plain stores for A/B): the output is
@@ -134,7 +134,8 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   constexpr int NPI = (NPC + 511) / 512;    // pieces per thread
   // epilogue LDS row pitch: 32 tiles + 2 — with 8-byte stores / reads, 34 cc mod 64 dwords puts
   // the 32 lanes of each ds_read_b64 group on 32 distinct bank pairs (a pitch of 36, needed by
-  // 16-byte stores, made every read 2-way conflicted)
+  // 16-byte stores, made every read 2-way conflicted): Winograd launches -2 % in the eager
+  // breakdown (DMX_WEPP=36 builds the old layout)
   constexpr int EPP = DMX_WEPP;
   constexpr int EPF = 16 * 32 * EPP;        // epilogue floats (one 32 x 32 pass, 16 positions)
   constexpr int LDSF = 2 * HBUF + 1024 > EPF ? 2 * HBUF + 1024 : EPF;
