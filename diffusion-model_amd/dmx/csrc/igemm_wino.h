@@ -49,6 +49,9 @@ namespace dmx {
 #define DMX_WDIAG 0
 #endif
 
+#ifndef DMX_WBAR2  // (A/B build) a barrier between the halo store and the A build
+#define DMX_WBAR2 0
+#endif
 #ifndef DMX_WEPP
 #define DMX_WEPP 34
 #endif
@@ -376,13 +379,13 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   };
   for (int c = 0; c < nch; ++c) {
     store_halo((c + 1) & 1, min(c + 1, nch - 1));  // c + 1 = nch: an unused store of the last chunk
-    // A barrier between the halo store and the A build.  Measured (tools/det_check.py, 12 repeats of
-    // a B = 128 forward): with the GroupNorm affine read from an LDS table in the store and no barrier
-    // here, GroupNorm-on-load convs were nondeterministic (some samples differed run to run, up to
-    // 6e-4 rel-L2); the LDS addresses of the store, the builds and the table are disjoint by
-    // construction and the root cause was not isolated.  This barrier alone, or the affine read from
-    // global memory alone, made every repeat bit-identical; both are kept (±0 measured).
-    __syncthreads();
+    // (No barrier here: buffer (c + 1) & 1 was last read by chunk c - 1's builds, which the previous
+    // iteration's closing barrier orders before this store, and this chunk's builds read the other
+    // buffer.  An earlier build with the GroupNorm affine in an LDS table was nondeterministic
+    // without a barrier here (tools/det_check.py); with the affine read from global memory the
+    // barrier is not needed — 0 of 9 repeats and 0 of 36 concurrent-process steps differ — and
+    // dropping it is +1.7-2.2 % per CFG step, 3 / 3 same-box rounds.  DMX_WBAR2=1 builds it back.)
+    if constexpr (DMX_WBAR2) __syncthreads();
     constexpr bool LATE = GNA == 2 || (W != 32 && GNA == 1);  // (register pressure: after m tile 0)
     if constexpr (!LATE) {
       load_halo(min(c + 2, nch - 1));
