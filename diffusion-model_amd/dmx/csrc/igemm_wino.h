@@ -49,6 +49,9 @@ namespace dmx {
 #define DMX_WDIAG 0
 #endif
 
+#ifndef DMX_WPRIO  // (A/B build) s_setprio 1 for waves 4-7 over the chunk loop
+#define DMX_WPRIO 0
+#endif
 #ifndef DMX_WBAR2  // (A/B build) a barrier between the halo store and the A build
 #define DMX_WBAR2 0
 #endif
@@ -377,6 +380,9 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
         }
       }
   };
+  if constexpr (DMX_WPRIO) {  // static priority for the second-dispatched half (MI355X_MICROARCH item 4)
+    if (wid >= 4) __builtin_amdgcn_s_setprio(1);
+  }
   for (int c = 0; c < nch; ++c) {
     store_halo((c + 1) & 1, min(c + 1, nch - 1));  // c + 1 = nch: an unused store of the last chunk
     // (No barrier here: buffer (c + 1) & 1 was last read by chunk c - 1's builds, which the previous
