@@ -749,14 +749,19 @@ struct Run {
   void tap(const std::string& name, const float* p, size_t count);
   std::string ck_layer;
   // DMX_CKSUM: one workspace checksum per layer, taken when the next layer's first kernel begins
+  // set by run_planned's real pass only: graph captures (dmx_sample_loop, dmx_step_profile) build
+  // their own Runs and never take checksums (the device slots may not exist yet, and a captured
+  // atomic would replay into stale slots)
+  bool cksum = false;
   void ck() {
     Cksum& c = cksum_state();
-    if (plan || m->ws_mem == nullptr || ck_layer.empty() || c.names.size() >= 1024) return;
+    if (!cksum || plan || c.dev == nullptr || m->ws_mem == nullptr || ck_layer.empty() || c.names.size() >= 1024)
+      return;
     cksum_kernel<<<1024, 256, 0, st>>>(static_cast<const unsigned*>(m->ws_mem), ws.off / 4, c.dev + c.names.size());
     c.names.push_back(ck_layer);
   }
   void begin(const std::string& kernel, double flops, double bytes) {
-    if (cksum_enabled() && layer != ck_layer) {
+    if (cksum && layer != ck_layer) {
       ck();
       ck_layer = layer;
     }
@@ -824,20 +829,15 @@ static int split_below() {
   }();
   return v;
 }
-// Smallest reduce_norm_kernel instance used (DMX_RN_MINKV, default 2).  The one-float4-per-thread
-// instance (KV = 1: the 4x4 C = 256 ResBlocks) gave run-to-run different outputs when a second
-// process shared the GPU (tools/conc_step.sh + DMX_CKSUM per-layer workspace checksums: the first
-// difference always after down3.0 / down3.1 / bot3, the three layers that use it; 9 of 9 runs in
-// one arm), while the KV = 2 instance on the same data — and splitk_reduce + norm_kernel — never
-// did (0 of 72).  No LDS or global hazard was found in its code; until the cause is known it is
-// not used.
-static int rn_minkv() {
-  static const int v = [] {
-    const char* e = std::getenv("DMX_RN_MINKV");
-    return e == nullptr ? 2 : std::atoi(e);
-  }();
-  return v;
-}
+// reduce_norm_kernel runs with at least two float4 per thread (KV >= 2; the 4x4 C = 256 ResBlocks,
+// 1024 float4 per sample, leave the second one idle).  The one-float4 instance (KV = 1) gave
+// run-to-run different outputs while a second process shared the GPU (tools/conc_step.sh +
+// DMX_CKSUM: first difference after down3.0 / down3.1 / bot3, its three users), the KV = 2 instance
+// on the same data never did (0 of 72).  The round-5 ISA review found no mechanism in the kernel
+// (no scratch, lgkmcnt(0) before both barriers, st_s read behind the second barrier, no
+// scalar loads of data, the producer covers every slab element — DMX_POISON), so the instance is not
+// compiled at all: no knob can select it.
+constexpr int RN_MIN_KV = 2;
 // DMX_RN_FUSE (race bisection): 0 = split-K slabs reduced by splitk_reduce_kernel + norm_kernel
 static bool rn_fuse_enabled() {
   static const bool v = [] {
@@ -914,6 +914,12 @@ struct GnLoad {
 // a config-3 shard of 64 samples per rank (128 with CFG) and the whole 128-sample batch (256) sum
 // every output in the same order (bit-identical latents, test_gpu_multi.py); below 64 the batch itself
 // (each kernel's partial-tile rules keep a small batch and its shards alike: test_gpu_poison.py).
+// Trade-off: batches far above 128 samples — a single-process B = 512 CFG batch of 1024
+// samples, a large training forward — take the split-K / Winograd-split / tile decisions of 128 samples
+// although their grids would fill the chip unsplit: more launches of the reduce kernels and split slabs
+// of splits * M * Cout floats (workspace linear in the batch, test_large_batch_class_is_shard_exact
+// bounds it) instead of whole-K tiles.  A coarser class above 128 would put a 64-per-rank shard and its
+// parent batch in different classes and lose config 3's bit-identical shards.
 static int dec_n(const Run& R, int N) {
   static const bool per_batch = [] {  // DMX_DEC_N=0 (A/B): decisions from the batch itself
     const char* e = std::getenv("DMX_DEC_N");
@@ -1076,8 +1082,15 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   if (src_mode == SRC_NCHW && epi == EPI_STATS && cw.taps == 9 && cw.phases == 1 && cw.cin == 4 && cw.cout == 64 &&
       W % 32 == 0 && seg == 32 && cw.bias == nullptr && R.m->kind != DMX_VAE && gn == nullptr) {
     // inc's first conv: direct fp32 conv of the NCHW input (kernels.h conv_in_kernel)
+    if (res != nullptr) throw Error(DMX_E_INTERNAL, "gemm: the direct input conv takes no residual");
+    if (ash != nullptr || asl != nullptr) throw Error(DMX_E_INTERNAL, "gemm: the direct input conv reads fp32 NCHW");
     if (defer != nullptr) *defer = Deferred{};  // whole K, no slabs
     if (R.plan) return H * W / 32;
+    if (check_args()) {  // (as every other GEMM path; the NCHW input is the caller's tensor, not checked)
+      check_range(R, cw.B, (size_t)cw.phases * cw.npad * cw.kpad * 4, "B");
+      check_range(R, out, (size_t)M * 64 * 4, "out");
+      check_range(R, rowpart, (size_t)N * (H * W / 32) * (64 / 32) * sizeof(float2), "rowpart");
+    }
     ConvInParams q;
     q.x = s.src0;
     q.creal = s.C0 ? s.C0 : s.C;
@@ -1353,14 +1366,13 @@ static void norm(Run& R, NormParams np, int N) {
 static void reduce_norm(Run& R, const Deferred& d, NormParams np, int n_src_samples) {
   if (R.plan) return;
   np.gexact = gelu_exact_flag(R);
-  const int kv = std::max(rn_minkv(), cdiv(np.HW * (np.C / 4), 1024));
+  const int kv = std::max(RN_MIN_KV, cdiv(np.HW * (np.C / 4), 1024));
   const int n_out = np.n_src > 0 ? 2 * n_src_samples : n_src_samples;
-  const int kvt = kv <= 1 ? 1 : kv <= 2 ? 2 : kv <= 4 ? 4 : RN_MAXV;
+  const int kvt = kv <= 2 ? 2 : kv <= 4 ? 4 : RN_MAXV;
   R.begin("reduce_norm_kernel<" + std::to_string(kvt) + ">", 0.0,
           4.0 * (double)n_src_samples * np.HW * np.C * (d.splits + (np.res ? 1 : 0)) +
               4.0 * (double)n_out * np.HW * np.C);
-  if (kv <= 1) reduce_norm_kernel<1><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
-  else if (kv <= 2) reduce_norm_kernel<2><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
+  if (kv <= 2) reduce_norm_kernel<2><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
   else if (kv <= 4) reduce_norm_kernel<4><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
   else reduce_norm_kernel<RN_MAXV><<<n_src_samples, 1024, 0, R.st>>>(d.partial, d.splits, d.bias, np);
   R.end();
@@ -1917,6 +1929,7 @@ static void run_planned(dmx_model* m, hipStream_t st, F&& body) {
     ck.names.clear();
   }
   Run R{m, st, false, m->ws};
+  R.cksum = cksum_enabled();
   body(R);
   if (m->ws.off != planned) throw Error(DMX_E_INTERNAL, "workspace plan / run mismatch");
   if (cksum_enabled()) {

@@ -399,6 +399,7 @@ constexpr int RN_MAXV = 8;  // float4 per thread
 template <int KV>
 __global__ __launch_bounds__(1024) void reduce_norm_kernel(const float* partial, int splits, const float* bias,
                                                            const NormParams p) {
+  static_assert(KV >= 2, "reduce_norm_kernel: the KV = 1 instance is retired (engine.hip RN_MIN_KV)");
   constexpr int SB = KV >= 16 ? 1 : 16 / KV;  // slabs per batch (<= 64 VGPRs of loads)
   const int s = blockIdx.x, tid = threadIdx.x;
   const int C4 = p.C >> 2, per = p.HW * C4;

@@ -37,10 +37,19 @@ def _diff():
         import sys
         path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "diff.py")
         spec = importlib.util.spec_from_file_location("diff", path)
+        if "diff" in sys.modules:  # (registered by another importer meanwhile)
+            return sys.modules["diff"]
         mod = importlib.util.module_from_spec(spec)
-        sys.modules.setdefault("diff", mod)
-        spec.loader.exec_module(mod)
-        return sys.modules["diff"]
+        # registered while it executes (its own imports may resolve "diff"), removed again if
+        # executing it fails, so no half-initialised module stays behind for a later `import diff`
+        sys.modules["diff"] = mod
+        try:
+            spec.loader.exec_module(mod)
+        except BaseException:
+            if sys.modules.get("diff") is mod:
+                del sys.modules["diff"]
+            raise
+        return mod
 
 
 def world() -> Tuple[int, int]:

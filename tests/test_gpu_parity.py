@@ -123,6 +123,29 @@ def test_bench_batch_forward_is_deterministic(model, cuda):
         assert torch.equal(e, outs[0][0]) and torch.equal(gm, outs[0][1])
 
 
+def test_large_batch_class_is_shard_exact(model, cuda):
+    """A 512-sample forward (a single-process B = 256 CFG batch) takes the 128-sample class decisions
+    (engine.hip dec_n): samples 0..127 come out bit-identical to a 128-sample forward of the same
+    inputs, and the workspace grows linearly with the batch (split slabs of splits * M * Cout floats;
+    ADVICE r4: bound it)."""
+    g = torch.Generator().manual_seed(512)
+    N = 512
+    x = torch.randn((N, 4, 32, 32), generator=g).to(cuda)
+    t = torch.randint(1, 1001, (N,), generator=g).to(cuda)
+    y = torch.randint(0, 4, (N,), generator=g).to(cuda)
+    vals = torch.rand((N, 12), generator=g).to(cuda)
+    mask = (torch.rand((N, 12), generator=g) > 0.5).float().to(cuda)
+    nm = model.native()
+    with torch.no_grad():
+        e128, g128 = model(x[:128], t[:128], y[:128], cond_vals=vals[:128], cond_mask=mask[:128])
+        ws128 = nm.workspace_bytes()
+        e512, g512 = model(x, t, y, cond_vals=vals, cond_mask=mask)
+        ws512 = nm.workspace_bytes()
+    print(f"[batch class] workspace 128: {ws128 / 2**30:.2f} GiB, 512: {ws512 / 2**30:.2f} GiB")
+    assert torch.equal(e512[:128], e128) and torch.equal(g512[:128], g128)
+    assert ws512 <= 4.2 * ws128
+
+
 def test_uncond_unet_golden(golden, cuda):
     from dmx import synth
     from models.unet import Unet
@@ -285,11 +308,14 @@ def test_cfg_step_full_batch_vs_oracle(model, cuda, unet_sd, prec):
     assert rel(out, exp) < TOL
 
 
-@pytest.mark.parametrize("B,hw", [(3, 32), (9, 32), (5, 16)])
+@pytest.mark.parametrize("B,hw", [(3, 32), (9, 32), (5, 16), (33, 32)])
 def test_cfg_step_ragged_batches_vs_oracle(model, cuda, unet_sd, B, hw):
     """Batches that are not a multiple of the low-resolution halo convs' whole-sample tiles (16
     samples of 4 x 4, 4 of 8 x 8: igemm_halo.h MS) — the last tile holds fewer samples, which stage
-    as zeros and whose rows the epilogue drops — and the split-K slab reduction behind them."""
+    as zeros and whose rows the epilogue drops — and the split-K slab reduction behind them.
+    B = 33 (a 66-sample CFG forward) is in the benchmark's batch class (>= 64 samples): its 3x3 convs
+    run the Winograd kernels, whose 8 x 8 blocks stack four samples, so the last block holds 2
+    (igemm_wino.h nsamp guards)."""
     import diff
     d = diff.Diffuser(1000, device=cuda)
     g = torch.Generator().manual_seed(300 + B)
@@ -333,6 +359,37 @@ def test_trajectory_T1000_golden(golden, model, vae, cuda, prec):
     assert ok, info
 
 
+def test_trajectory_T1000_B32_winograd_class_golden(golden, model, vae, cuda):
+    """T=1000 CFG trajectory at B=32 (a 64-sample CFG forward: the batch class whose 3x3 convs run the
+    Winograd kernels bench.py times) on the reference's own draws (tests/golden/make_golden_r5.py,
+    diff.py:326-344 loop of denoise_cond): latents at t = 900 / 500 / 100 (samples 0..7) and after
+    t = 1 (all 32) within 1e-4 rel-L2, decoded uint8 images of samples 0..5 within +-1 LSB on <= 0.1 %.
+    x3 mode (the default, fp32 semantics)."""
+    import diff
+    g = golden("traj_T1000_B32.npz")
+    nm = model.native()
+    assert nm.precision == "x3"
+    B, sub = int(g["y"].shape[0]), int(g["sub"])
+    d = diff.Diffuser(1000, device=cuda)
+    y = torch.from_numpy(g["y"]).to(cuda)
+    vals, mask = torch.from_numpy(g["vals"]).to(cuda), torch.from_numpy(g["mask"]).to(cuda)
+    torch.manual_seed(int(g["seed"]))
+    x = torch.randn((B, 4, 32, 32)).to(cuda)
+    errs = {}
+    for i in range(1000, 0, -1):
+        t = torch.full((B,), i, dtype=torch.long, device=cuda)
+        x = d.denoise_cond(model, x, t, y=y, guidance_scale=3.0, null_label=0, cond_vals=vals, cond_mask=mask)
+        if i in (900, 500, 100):
+            errs[i] = rel(x[:sub], g[f"x_{i}"])
+    errs[1] = rel(x, g["x_final"])
+    n_img = int(g["u8"].shape[0])
+    u8 = vae.decode_uint8(x[:n_img].contiguous()).cpu().numpy()
+    ok, info = u8_close(u8, g["u8"])
+    print(f"[trajectory T=1000 B=32 x3] latents rel-L2 vs reference {errs}, pixels {info}")
+    assert all(e < 1e-4 for e in errs.values()), errs
+    assert ok, info
+
+
 def test_sample_latent_cond_T20_28_path(golden, model, vae, cuda):
     """z_shape=None (28x28 latents via the replayed encode draw), pixels via PIL, and z_shape given."""
     import diff
@@ -364,19 +421,21 @@ def test_uncond_sample_latent_T100_golden(golden, cuda):
     assert rel(z, g["latent"]) < 1e-4
 
 
-def test_graph_loop_equals_eager_and_is_deterministic(model, cuda):
+@pytest.mark.parametrize("B", [4, 64])
+def test_graph_loop_equals_eager_and_is_deterministic(model, cuda, B):
     """Device-noise mode: hipGraph replay == eager launches, bit for bit, and reruns are identical
-    (19 steps: two launches of the 8-step graph and three of the one-step graph)."""
+    (19 steps: two launches of the 8-step graph and three of the one-step graph).  B = 64 is the
+    benchmark's timed region (bench.py: the 8-step graph at B = 64 — Winograd convs, Philox noise,
+    cond-MLP rows computed once per graph)."""
     from dmx import engine  # noqa: F401
     import diff
     d = diff.Diffuser(1000, device=cuda)
     nm = model.native()
-    B = 4
     g = torch.Generator().manual_seed(2)
     x0 = torch.randn((B, 4, 32, 32), generator=g).to(cuda)
-    y = torch.tensor([1, 2, 3, 1], device=cuda)
+    y = torch.tensor([1 + i % 3 for i in range(B)], device=cuda)
     vals = torch.rand((B, 12), generator=g).to(cuda)
-    mask = torch.ones((B, 12), device=cuda)
+    mask = (torch.rand((B, 12), generator=g) > 0.3).float().to(cuda) if B > 4 else torch.ones((B, 12), device=cuda)
     tables = d.coef_tables(cuda, True)
     outs = []
     for use_graph in (True, False, True):
