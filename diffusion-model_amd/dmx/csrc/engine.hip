@@ -987,29 +987,40 @@ static bool wino_split_enabled() {
   }();
   return v;
 }
-// DMX_WINO_MASK (bisection aid): bit 0 / 1 / 2 allow the Winograd conv at W = 8 / 16 / 32 (default 7)
+// DMX_WINO_F16 (A/B): 1 (default) the fp16 mode (config 4, precision 2) runs the Winograd convs too
+// (X1 instances: U hi and V rounded to f16, one MFMA per product); 0 keeps its direct kernels.
+static bool wino_f16_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("DMX_WINO_F16");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return v;
+}
+// DMX_WINO_MASK (bisection aid / A/B): bit 0 / 1 / 2 / 3 allow the Winograd conv at W = 8 / 16 / 32 / 4
+// (default 15)
 static int wino_mask() {
   static const int v = [] {
     const char* e = std::getenv("DMX_WINO_MASK");
-    return e == nullptr ? 7 : std::atoi(e);
+    return e == nullptr ? 15 : std::atoi(e);
   }();
   return v;
 }
 // Winograd plan of a 3x3 conv given an fp32 source: 0 = not applicable, else the K split count
 // (1 = whole K) and *cps = 16-channel chunks per split.  Blocks: 64 tiles (8 rows of a 32-wide map,
-// one 16 x 16 sample, four 8 x 8 samples — the last block of a batch that is not a multiple of 4
-// holds fewer) x 64 output channels.  The split count is a function of the conv's shape and of a
+// one 16 x 16 sample, four 8 x 8 samples or sixteen 4 x 4 samples — the last block of a batch that
+// is not a multiple of 4 / 16 holds fewer) x 64 output channels.  The split count is a function of the conv's shape and of a
 // coarse batch class only: it is planned for a reference batch of 128 samples (the benchmark's CFG
 // batch) when the batch has >= 64 samples, of 2 samples below that (single-sample and small batches
 // keep a full grid).  A batch and its shards in the same class sum every output in the same order
 // (bit-identical results: test_gpu_poison.py's B = 5 vs 3 + 2; a 64-per-rank shard plans as the bench).
 static int wino_plan(const Run& R, int src_C, int N, int H, int W, const ConvW& cw, int* cps) {
   // (U-Net only: the VAE decoder keeps its per-sample-tiled direct convs, Run::tile_n)
-  if (!wino_enabled() || R.m->prec != 1 || R.m->kind == DMX_VAE || R.tile_n > 0 || cw.Uh == nullptr ||
+  if (!wino_enabled() || R.m->prec < 1 || (R.m->prec == 2 && !wino_f16_enabled()) || R.m->kind == DMX_VAE ||
+      R.tile_n > 0 || cw.Uh == nullptr ||
       cw.phases != 1 || cw.taps != 9)
     return 0;
-  if (!((W == 32 && H % 8 == 0) || (W == 16 && H == 16) || (W == 8 && H == 8))) return 0;
-  if (!((wino_mask() >> (W == 8 ? 0 : W == 16 ? 1 : 2)) & 1)) return 0;
+  if (!((W == 32 && H % 8 == 0) || (W == 16 && H == 16) || (W == 8 && H == 8) || (W == 4 && H == 4))) return 0;
+  if (!((wino_mask() >> (W == 8 ? 0 : W == 16 ? 1 : W == 32 ? 2 : 3)) & 1)) return 0;
   if (src_C % 16 != 0 || cw.cout % 64 != 0 || (size_t)16 * cw.cout * src_C * 2 >= ((size_t)1 << 31)) return 0;
   const int nref = dec_n(R, N) >= 64 ? 128 : 2;
   const int blocks = cdiv(nref * H * W, 256) * (cw.cout / 64), nch = src_C / 16;
@@ -1022,6 +1033,7 @@ static int wino_plan(const Run& R, int src_C, int N, int H, int W, const ConvW& 
     cp = cdiv(nch, sp);
     sp = cdiv(nch, cp);
   }
+  if (W == 4 && sp == 1) return 0;  // (4 x 4: split-K instances only; sixteen samples per block)
   if (cps != nullptr) *cps = cp;
   return sp;
 }
@@ -1289,9 +1301,10 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
       check_range(R, cw.Uh, xp.u_bytes, "U hi");
       check_range(R, cw.Ul, xp.u_bytes, "U lo");
       const int e = splits > 1 ? (int)EPI_PARTIAL : (int)EPI_STATS;
-      std::snprintf(nm, sizeof nm, "wino_kernel<%d, %d, %d>", W, gna, e);
+      if (x1) std::snprintf(nm, sizeof nm, "wino_kernel<%d, %d, %d, 1>", W, gna, e);
+      else std::snprintf(nm, sizeof nm, "wino_kernel<%d, %d, %d>", W, gna, e);
       R.begin(nm, flops, bytes + (splits > 1 ? 4.0 * splits * M * cw.cout : 0.0));
-      launch_wino(e, W, gna, xp, dim3(cdiv(M, 256), cw.cout / 64, splits), R.st);
+      launch_wino(e, W, gna, x1 ? 1 : 0, xp, dim3(cdiv(M, 256), cw.cout / 64, splits), R.st);
       R.end();
       HIPCHK(hipGetLastError());
       if (splits == 1 || (defer != nullptr && defer->fused)) return rrows;

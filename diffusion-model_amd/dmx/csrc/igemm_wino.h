@@ -29,6 +29,8 @@
 //   * B (U) fragments come straight from the fragment-ordered planes into registers (1 KB coalesced
 //     per fragment, L2-resident), each reloaded for the next chunk right after its last MFMA;
 //   * one barrier per chunk (halo double buffer).
+// X1 = 1 (config 4, BASELINE configs[3]): U hi and V rounded to f16 once, one MFMA per product
+// (fp32 accumulate), transforms in fp32 as in the x3 instances.
 // Epilogue: in four passes of (32 tiles x 32 channels) the 16 position accumulators go through LDS,
 // every thread applies Aᵀ M A to two tiles of one channel in a fixed order, stores the 2x2 pixels
 // (NHWC fp32) and the GroupNorm (sum, sum of squares) partials of 16-pixel x 32-channel groups
@@ -109,34 +111,41 @@ static __global__ void wino_pack_kernel(const float* B, int kpad, int cin, int c
 
 // Geometry.  W = 32: a block is 8 output rows of one sample (4 tile rows x 16); W = 16: one whole
 // sample (8 x 8 tiles); W = 8: four whole samples (4 x 4 tiles each), their halos stacked at a pitch
-// of PS = 11 halo rows (the 11th row is padding).  Halo pixel (row, col) lives at float offset
-// (row * 2 + col % 2) * RP * 4 + (col / 2) * 20 + channel: even / odd columns in separate planes,
+// of PS = 11 halo rows (the 11th row is padding); W = 4: sixteen whole samples.  Halo pixel (row, col)
+// of stacked sample s lives at float offset s * SQ + (row * 2 + col % 2) * RP * 4 + (col / 2) * 20 + channel: even / odd columns in separate planes,
 // 20 floats (16 channels + 4 pad) per pixel, RP 16-byte units per plane row.  A fragment row (tile)
 // of lane fr then reads at (s * PS + 2 ty) * 8 RP + 5 tx units + const, and RP is chosen so that each
 // 16-lane group of ds_read_b128 ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32) hits 16 distinct
 // 16-byte bank slots: W = 32 (2 tile rows per 32 tiles) needs 4 RP = 0 mod 16 (RP = 88), W = 16
 // (4 tile rows) 4 RP = 8 mod 16 (RP = 46), W = 8 (2 samples x 4 tile rows, PS = 11) 2 RP = 4 mod 16
-// (RP = 26).
+// (RP = 26).  W = 4: sixteen whole samples (2 x 2 tiles each), 6 halo rows each; no whole-row pitch
+// spreads the 16 lanes of a group over 16 slots there, so a stacked sample starts every SQ = 218
+// units (> 12 RP = 216, RP = 18: 4 RP = 8 mod 16), which does.
 // EPI = EPI_STATS: the conv output and its GroupNorm partials; EPI_PARTIAL (grid.z = K splits over
 // 16-channel chunks, P.g.ksplit chunks each): the split's transformed partial output to slab z,
 // reduced in split order by reduce_norm_kernel / splitk_reduce_kernel (the output transform is
 // linear, so transforming each split's partial sums and adding the pixels equals transforming the
 // total).
-template <int W, int GNA, int EPI = EPI_STATS>
+template <int W, int GNA, int EPI = EPI_STATS, int X1 = 0>
 __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   static_assert(EPI == EPI_STATS || EPI == EPI_PARTIAL, "Winograd epilogues");
-  static_assert(W == 32 || W == 16 || W == 8, "Winograd conv: image width 8, 16 or 32");
+  static_assert(W == 32 || W == 16 || W == 8 || W == 4, "Winograd conv: image width 4, 8, 16 or 32");
+  static_assert(W != 4 || GNA == 0, "W = 4: no GroupNorm-on-load instances");
   const IgemmParams& p = P.g;
   constexpr int TW = W / 2;                       // tiles per tile row
-  constexpr int SPB = W == 8 ? 4 : 1;             // samples per block
+  constexpr int SPB = W == 8 ? 4 : W == 4 ? 16 : 1;  // samples per block
   constexpr int TPS = 64 / SPB;                   // tiles per sample in the block
   constexpr int HRS = (W == 32 ? 8 : W) + 2;      // halo rows per sample
   constexpr int PS = W == 8 ? 11 : HRS;           // halo row pitch between stacked samples
   constexpr int HR = SPB * PS, HC = W + 2;        // halo rows / columns
-  constexpr int RP = W == 32 ? 88 : W == 16 ? 46 : 26;  // parity-plane row pitch in 16-byte units
-  constexpr int HBUF = HR * 2 * RP * 4;           // floats per halo buffer
+  constexpr int RP = W == 32 ? 88 : W == 16 ? 46 : W == 8 ? 26 : 18;  // parity-plane row pitch, 16-byte units
+  constexpr int SQ = W == 4 ? 218 * 4 : PS * 8 * RP;  // floats per stacked sample (W = 4: not whole rows)
+  constexpr int HBUF = SPB * SQ;                  // floats per halo buffer
+  // W = 4: the halo ring of every (whole) sample is zero padding — written once, both buffers, before
+  // the loop; the chunks stage the 4 x 4 interiors only (1024 pieces: 2 per thread instead of 5)
+  constexpr bool RING0 = W == 4;
   constexpr int CK = 16;                    // channels per chunk
-  constexpr int NPC = HR * HC * (CK / 4);   // float4 pieces per chunk
+  constexpr int NPC = RING0 ? SPB * W * W * (CK / 4) : HR * HC * (CK / 4);  // float4 pieces per chunk
   constexpr int NPI = (NPC + 511) / 512;    // pieces per thread
   // epilogue LDS row pitch: 32 tiles + 2 — with 8-byte stores / reads, 34 cc mod 64 dwords puts
   // the 32 lanes of each ds_read_b64 group on 32 distinct bank pairs (a pitch of 36, needed by
@@ -167,13 +176,15 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   for (int k = 0; k < NPI; ++k) {
     const int e = tid + 512 * k;
     const int h = e >> 2, q = e & 3;
-    const int hy = h / HC, hx = h - hy * HC;
-    const int sh = hy / PS, ry = hy - sh * PS;  // stacked sample, halo row inside it
+    // stacked sample, halo row inside it, halo column (RING0: interior pixel h of the block's samples)
+    const int sh = RING0 ? h >> 4 : (h / HC) / PS;
+    const int ry = RING0 ? ((h >> 2) & 3) + 1 : h / HC - sh * PS;
+    const int hx = RING0 ? (h & 3) + 1 : h - (h / HC) * HC;
     const int y = y0 + ry - 1, x = hx - 1;
     const bool ok = e < NPC && ry < HRS && y >= 0 && y < p.H && x >= 0 && x < W && nsmp + sh < nsamp;
     hoff[k] = ok ? ((((nsmp + sh) * p.H + y) * W + x) * C + q * 4) : -1;
     // pieces past the halo store to a scratch slot of their own (no divergent branch around the store)
-    hls[k] = e < NPC ? ((hy * 2 + (hx & 1)) * RP * 4 + (hx >> 1) * 20 + q * 4) : 2 * HBUF + (tid & 255) * 4;
+    hls[k] = e < NPC ? (sh * SQ + (ry * 2 + (hx & 1)) * RP * 4 + (hx >> 1) * 20 + q * 4) : 2 * HBUF + (tid & 255) * 4;
   }
   const __amdgpu_buffer_rsrc_t rA = rsrc_of(p.src.src0, P.a_bytes);
   const __amdgpu_buffer_rsrc_t rRes = rsrc_of(GNA == 2 ? (const void*)P.gn_res : (const void*)p.src.src0, P.a_bytes);
@@ -263,7 +274,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   auto load_b = [&](int q, int n, int c) {
     const int cc = c < 0 ? cnext : c;
     bh[q][n] = bload_h8(rUh, voff, ub[q][n] + (cbeg + cc) * 1024);
-    bl[q][n] = bload_h8(rUl, voff, ub[q][n] + (cbeg + cc) * 1024);
+    if constexpr (!X1) bl[q][n] = bload_h8(rUl, voff, ub[q][n] + (cbeg + cc) * 1024);
   };
 
   // ---- A fragments: rows (Bᵀ row wi) and columns (B columns of positions 2jp, 2jp + 1)
@@ -281,7 +292,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
 #pragma unroll
   for (int mb = 0; mb < 2; ++mb) {
     const int t = 32 * mb + fr, st = t / TPS, tt = t - st * TPS, ty = tt / TW, tx = tt - ty * TW;
-    tb[mb] = (st * PS + 2 * ty) * 8 * RP + tx * 20 + 8 * fh;
+    tb[mb] = st * SQ + 2 * ty * 8 * RP + tx * 20 + 8 * fh;
   }
   half8 ah[2], al[2];  // [position] of the current m tile
   auto build = [&](int buf, int mb) {
@@ -317,14 +328,19 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
       for (int e = 0; e < 4; e += 2) {
         const float a0 = T[0][e] - T[1][e], a1 = T[0][e + 1] - T[1][e + 1];
         const float b0 = fmaf(T[2][e], sb, T[1][e]), b1 = fmaf(T[2][e + 1], sb, T[1][e + 1]);
-        split2u(a0, a1, vh[0][2 * h + e / 2], vl[0][2 * h + e / 2]);
-        split2u(b0, b1, vh[1][2 * h + e / 2], vl[1][2 * h + e / 2]);
+        if constexpr (X1) {  // config 4: V rounded to f16 once, no lo part
+          vh[0][2 * h + e / 2] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){a0, a1}, half2v));
+          vh[1][2 * h + e / 2] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){b0, b1}, half2v));
+        } else {
+          split2u(a0, a1, vh[0][2 * h + e / 2], vl[0][2 * h + e / 2]);
+          split2u(b0, b1, vh[1][2 * h + e / 2], vl[1][2 * h + e / 2]);
+        }
       }
     }
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       ah[q] = __builtin_bit_cast(half8, (u32x4){vh[q][0], vh[q][1], vh[q][2], vh[q][3]});
-      al[q] = __builtin_bit_cast(half8, (u32x4){vl[q][0], vl[q][1], vl[q][2], vl[q][3]});
+      if constexpr (!X1) al[q] = __builtin_bit_cast(half8, (u32x4){vl[q][0], vl[q][1], vl[q][2], vl[q][3]});
     }
   };
 
@@ -342,7 +358,11 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   // in the loop's steady-state order (halo loads older than U loads), so the counted vmcnt waits the
   // compiler derives at the loop head (merged over entry and back edge) let the store of the halo
   // retire only the halo loads instead of draining the U fragments too
+  if constexpr (RING0) {  // zero both halo buffers once (the rings are never stored again)
+    for (int i = tid; i < 2 * HBUF / 4; i += 512) *reinterpret_cast<floatx4*>(lds + 4 * i) = floatx4{0.f, 0.f, 0.f, 0.f};
+  }
   load_halo(0);
+  if constexpr (RING0) __syncthreads();
   store_halo(0, 0);
   load_halo(min(1, nch - 1));
 #pragma unroll
@@ -370,8 +390,10 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
         if constexpr (DMX_WDIAG & 1) {
           asm volatile("" ::"v"(al[q]), "v"(ah[q]), "v"(bh[q][n]), "v"(bl[q][n]));
         } else {
-          acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[q], bh[q][n], acc[q][i][n], 0, 0, 0);
-          acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[q], bl[q][n], acc[q][i][n], 0, 0, 0);
+          if constexpr (!X1) {
+            acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[q], bh[q][n], acc[q][i][n], 0, 0, 0);
+            acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[q], bl[q][n], acc[q][i][n], 0, 0, 0);
+          }
           acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[q], bh[q][n], acc[q][i][n], 0, 0, 0);
         }
         if (reload) {

@@ -3,26 +3,36 @@
 #include "launch.h"
 
 #include <algorithm>
+#include <stdexcept>
 
 namespace dmx {
 
-template <int W, int EPI>
+template <int W, int EPI, int X1>
 static void go(int gna, const X3Params& p, dim3 grid, hipStream_t st) {
-  if (gna == 1) wino_kernel<W, 1, EPI><<<grid, 512, 0, st>>>(p);
-  else if (gna == 2) wino_kernel<W, 2, EPI><<<grid, 512, 0, st>>>(p);
-  else wino_kernel<W, 0, EPI><<<grid, 512, 0, st>>>(p);
+  // (GNA = 2, the residual GELU(x + GN) on load, is never dispatched: engine.hip wino_gna_pays — it
+  // lost 10-42 us per conv against a norm pass — so its instances are not built)
+  if (gna == 1) wino_kernel<W, 1, EPI, X1><<<grid, 512, 0, st>>>(p);
+  else if (gna == 0) wino_kernel<W, 0, EPI, X1><<<grid, 512, 0, st>>>(p);
+  else throw std::runtime_error("launch_wino: no GroupNorm-residual-GELU instances");
 }
 
-template <int EPI>
+template <int EPI, int X1>
 static void by_w(int w, int gna, const X3Params& p, dim3 grid, hipStream_t st) {
-  if (w == 32) go<32, EPI>(gna, p, grid, st);
-  else if (w == 16) go<16, EPI>(gna, p, grid, st);
-  else go<8, EPI>(gna, p, grid, st);
+  if (w == 32) go<32, EPI, X1>(gna, p, grid, st);
+  else if (w == 16) go<16, EPI, X1>(gna, p, grid, st);
+  else if (w == 8) go<8, EPI, X1>(gna, p, grid, st);
+  else if (EPI == EPI_PARTIAL && gna == 0) wino_kernel<4, 0, EPI_PARTIAL, X1><<<grid, 512, 0, st>>>(p);
+  else throw std::runtime_error("launch_wino: W = 4 runs split-K without GroupNorm-on-load only");
 }
 
-void launch_wino(int epi, int w, int gna, const X3Params& p, dim3 grid, hipStream_t st) {
-  if (epi == EPI_PARTIAL) by_w<EPI_PARTIAL>(w, gna, p, grid, st);
-  else by_w<EPI_STATS>(w, gna, p, grid, st);
+void launch_wino(int epi, int w, int gna, int x1, const X3Params& p, dim3 grid, hipStream_t st) {
+  if (x1) {
+    if (epi == EPI_PARTIAL) by_w<EPI_PARTIAL, 1>(w, gna, p, grid, st);
+    else by_w<EPI_STATS, 1>(w, gna, p, grid, st);
+  } else {
+    if (epi == EPI_PARTIAL) by_w<EPI_PARTIAL, 0>(w, gna, p, grid, st);
+    else by_w<EPI_STATS, 0>(w, gna, p, grid, st);
+  }
 }
 
 void launch_wino_pack(const float* B, int kpad, int cin, int cout, float scale, _Float16* uh, _Float16* ul,

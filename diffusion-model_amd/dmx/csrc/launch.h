@@ -42,9 +42,10 @@ void launch_halo_ms(int epi, int bn, int w, int sa, int x1, const X3Params& p, d
 // chunk-staged variant (igemm_halo_cs_kernel): BN = 64, all nine taps of a chunk's B slice in LDS.
 void launch_halo_cs(int epi, int w, int sa, int x1, const X3Params& p, dim3 grid, hipStream_t st);
 // Winograd F(2x2, 3x3) split-precision 3x3 conv (igemm_wino.h), 64 tiles (256 pixels) x 64 channels
-// per block, w in {8, 16, 32}, gna as launch_halo; k_wino.hip.  epi EPI_STATS (GroupNorm partials:
-// HW / 16 rows per sample) or EPI_PARTIAL (grid.z = K splits over 16-channel chunks).
-void launch_wino(int epi, int w, int gna, const X3Params& p, dim3 grid, hipStream_t st);
+// per block, w in {4, 8, 16, 32} (4: EPI_PARTIAL, gna 0 only), gna as launch_halo, x1 = 1 the fp16
+// (config 4) instances; k_wino.hip.  epi EPI_STATS (GroupNorm partials: HW / 16 rows per sample) or
+// EPI_PARTIAL (grid.z = K splits over 16-channel chunks).
+void launch_wino(int epi, int w, int gna, int x1, const X3Params& p, dim3 grid, hipStream_t st);
 // U = G g Gᵀ of a packed fp32 3x3 weight ([npad][kpad], k = tap * cin + c), scaled, split, fragment order
 void launch_wino_pack(const float* B, int kpad, int cin, int cout, float scale, _Float16* uh, _Float16* ul,
                       hipStream_t st);
