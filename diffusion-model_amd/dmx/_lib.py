@@ -105,6 +105,7 @@ SIGNATURES = [
     ("dmx_debug_num_taps", _I, [_P]),
     ("dmx_debug_tap", _I, [_P, _I, ctypes.c_char_p, _I, ctypes.POINTER(_I64), _P, _P]),
     ("dmx_step_profile", _I, [_P, ctypes.POINTER(StepArgs), ctypes.POINTER(KernelRecord), _I, ctypes.POINTER(_I), _P]),
+    ("dmx_diag_wino_stamps", _I, [_P, _I]),
 ]
 
 _lib = None

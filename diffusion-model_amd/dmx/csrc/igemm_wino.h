@@ -68,6 +68,35 @@ namespace dmx {
 #ifndef DMX_WNT
 #define DMX_WNT 1
 #endif
+#ifndef DMX_WNT_PART  // (A/B build) the hint on EPI_PARTIAL split slabs too (read back at once by the reduce)
+#define DMX_WNT_PART 1
+#endif
+
+// Diagnostic builds only (-DDMX_WSTAMP=1, k_wino.hip's dmx_diag_wino_stamps reads them): wave 0 of
+// every block records s_memtime at kernel start, after the prologue barrier, after the chunk loop
+// and at the end, plus the hardware id (XCC, CU), into g_wstamp[launch slot][block] — timing only,
+// no output value depends on them (MI355X_MICROARCH.md DVFS note 6).
+#ifndef DMX_WSTAMP
+#define DMX_WSTAMP 0
+#endif
+#if DMX_WSTAMP
+constexpr int WSTAMP_SLOTS = 32, WSTAMP_BLOCKS = 2048;
+__device__ unsigned long long g_wstamp[WSTAMP_SLOTS * WSTAMP_BLOCKS * 5];
+DMX_DEV void wstamp(int slot, int k) {
+  if (threadIdx.x == 0 && slot >= 0 && slot < WSTAMP_SLOTS) {
+    const int b = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    if (b < WSTAMP_BLOCKS) {
+      unsigned long long* q = g_wstamp + ((size_t)slot * WSTAMP_BLOCKS + b) * 5;
+      q[k] = __builtin_amdgcn_s_memtime();
+      if (k == 0) q[4] = ((unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) << 32) |
+                         (unsigned)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+    }
+  }
+}
+#define WSTAMP(k) wstamp(P.dslot, k)
+#else
+#define WSTAMP(k)
+#endif
 
 // U = G g Gᵀ of one 3x3 kernel for position (i, j), in double (exact products of ½-multiples).
 DMX_DEV double wino_u(const double (&g)[3][3], int i, int j) {
@@ -156,6 +185,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   constexpr int LDSF = 2 * HBUF + 1024 > EPF ? 2 * HBUF + 1024 : EPF;
   __shared__ __attribute__((aligned(16))) float lds[LDSF];
 
+  WSTAMP(0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wi = wid >> 1, jp = wid & 1;
@@ -370,6 +400,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
 #pragma unroll
     for (int n = 0; n < 2; ++n) load_b(q, n, 0);
   __syncthreads();
+  WSTAMP(1);
 
   // Per chunk c (halo buffers alternate; U fragments rolling in registers):
   //   store chunk c + 1's halo (registers loaded one chunk earlier) -> buffer (c + 1) & 1, issue chunk
@@ -433,6 +464,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
 
   // ---- epilogue: Aᵀ M A per tile, four passes of 32 tiles x 32 channels through LDS
   __syncthreads();  // (the halo buffers become the epilogue's staging area)
+  WSTAMP(2);
   const int HW16 = HW / 16, nseg = p.Cout / 32;
   const int tile0 = (m0 - nsmp * HW) / 4;  // first tile of the block inside its sample
   const int cc = tid & 31, tp = tid >> 5;  // output task: channel cc, tiles 2 tp, 2 tp + 1
@@ -492,7 +524,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
             const int oy = y0 + 2 * ty + r, ox = 2 * tx + s;
             if (!(DMX_WDIAG & 24) && nsmp + st < nsamp) {
               float* a = &dst[(((size_t)(nsmp + st) * p.H + oy) * W + ox) * p.Cout + col];
-              if constexpr (DMX_WNT) __builtin_nontemporal_store(y, a);
+              if constexpr (DMX_WNT && (EPI == EPI_STATS || DMX_WNT_PART)) __builtin_nontemporal_store(y, a);
               else *a = y;
             }
             ys[4 * e + 2 * r + s] = y;
@@ -522,6 +554,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
       }
       __syncthreads();
     }
+  WSTAMP(3);
 }
 
 }  // namespace dmx

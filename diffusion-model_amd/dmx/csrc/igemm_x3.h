@@ -50,6 +50,7 @@ struct X3Params {
   const _Float16* Uh;
   const _Float16* Ul;
   unsigned u_bytes;          // bytes of one U plane (16 * Cout * Cin f16)
+  int dslot;                 // diagnostic builds (DMX_WSTAMP): stamp slot of this launch, else unused
 };
 
 

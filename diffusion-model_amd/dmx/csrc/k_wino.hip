@@ -4,8 +4,13 @@
 
 #include <algorithm>
 #include <stdexcept>
+#include <vector>
 
 namespace dmx {
+
+#if DMX_WSTAMP
+static int g_wstamp_next = 0;  // stamp slot of the next Winograd launch (reset by dmx_diag_wino_stamps)
+#endif
 
 template <int W, int EPI, int X1>
 static void go(int gna, const X3Params& p, dim3 grid, hipStream_t st) {
@@ -25,7 +30,13 @@ static void by_w(int w, int gna, const X3Params& p, dim3 grid, hipStream_t st) {
   else throw std::runtime_error("launch_wino: W = 4 runs split-K without GroupNorm-on-load only");
 }
 
-void launch_wino(int epi, int w, int gna, int x1, const X3Params& p, dim3 grid, hipStream_t st) {
+void launch_wino(int epi, int w, int gna, int x1, const X3Params& p0, dim3 grid, hipStream_t st) {
+  X3Params p = p0;
+#if DMX_WSTAMP
+  p.dslot = g_wstamp_next++;
+#else
+  p.dslot = -1;
+#endif
   if (x1) {
     if (epi == EPI_PARTIAL) by_w<EPI_PARTIAL, 1>(w, gna, p, grid, st);
     else by_w<EPI_STATS, 1>(w, gna, p, grid, st);
@@ -42,3 +53,23 @@ void launch_wino_pack(const float* B, int kpad, int cin, int cout, float scale, 
 }
 
 }  // namespace dmx
+
+// Diagnostic (DMX_WSTAMP builds): copy the Winograd stamp table (slots x 2048 blocks x {t0, t1, t2,
+// t3, hw id}) to the host; returns the number of uint64 copied, 0 in regular builds.
+extern "C" int dmx_diag_wino_stamps(unsigned long long* host, int cap) {
+#if DMX_WSTAMP
+  if (host == nullptr) {  // reset: the next launch stamps into slot 0, the table is cleared
+    dmx::g_wstamp_next = 0;
+    static const std::vector<unsigned long long> zeros(sizeof(dmx::g_wstamp) / 8, 0ull);
+    return hipMemcpyToSymbol(HIP_SYMBOL(dmx::g_wstamp), zeros.data(), sizeof(dmx::g_wstamp)) == hipSuccess ? 0 : -1;
+  }
+  const size_t n = std::min<size_t>((size_t)cap, sizeof(dmx::g_wstamp) / 8);
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(dmx::g_wstamp), n * 8, 0, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return (int)n;
+#else
+  (void)host;
+  (void)cap;
+  return 0;
+#endif
+}

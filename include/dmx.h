@@ -212,6 +212,12 @@ int dmx_debug_enable(dmx_model* m, int on);
 int dmx_debug_num_taps(const dmx_model* m);
 int dmx_debug_tap(dmx_model* m, int i, char* name_out, int cap, int64_t* count_out, float* dst, void* stream);
 
+/* ---- timing diagnostic (libraries built with -DDMX_WSTAMP=1 only; regular builds return 0): the
+ * per-block s_memtime stamps of the Winograd conv launches ({start, after prologue, after chunk loop,
+ * end, hardware id} x 2048 blocks x 32 launch slots, uint64) copied to host memory; returns the count
+ * copied or -1; host == NULL resets the table and the launch counter.  tools/wino_stamps.py reads them. */
+int dmx_diag_wino_stamps(unsigned long long* host, int cap);
+
 /* Bytes of device workspace currently held by a model (diagnostics). */
 int64_t dmx_model_workspace_bytes(const dmx_model* m);
 

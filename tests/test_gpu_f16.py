@@ -11,6 +11,7 @@ Stated tolerances (measured on MI355X, synthetic weights, this repo's goldens, i
   * one CFG step at B=64 (x_{t-1}) rel-L2 <= 1e-4           [1.4e-5]
   * T=1000 CFG trajectory latents rel-L2 <= 2e-3            [5.3e-4 @900 .. 7.1e-4 final]
     and its decoded uint8 pixels |diff| <= 2 on <= 5 %      [max 1, 1.7 %]
+    (B=2: the direct kernels; B=32: the fp16 Winograd convs of the bench batch class)
   * VAE decode (decoder in f16) rel-L2 <= 1e-3; uint8 |diff| <= 2 on <= 5 %   [1.3e-4; max 1, 1.4 %]
 (the fp32-semantics default "x3" keeps the north star's 1e-4 on latents: tests/test_gpu_parity.py)
 """
@@ -107,6 +108,58 @@ def test_f16_trajectory_T1000(golden, model16, vae_sd, cuda):
     for k, v in errs.items():
         assert v < TOL_TRAJ, (k, v)
     assert du.max() <= 2 and (du > 0).mean() <= 0.05
+
+
+def test_f16_trajectory_T1000_B32_winograd_class(golden, model16, vae_sd, cuda):
+    """The T=1000 trajectory at B=32 (a 64-sample CFG forward: the batch class whose 3x3 convs run the
+    fp16 Winograd instances, igemm_wino.h X1 = 1, as the config-4 bench leg does) against the
+    reference's own B=32 trajectory (tests/golden/make_golden_r5.py): the same bounds as above."""
+    import diff
+    from models.vae import VAE
+    g = golden("traj_T1000_B32.npz")
+    B, sub = int(g["y"].shape[0]), int(g["sub"])
+    d = diff.Diffuser(1000, device=cuda)
+    y = torch.from_numpy(g["y"]).to(cuda)
+    vals, mask = torch.from_numpy(g["vals"]).to(cuda), torch.from_numpy(g["mask"]).to(cuda)
+    torch.manual_seed(int(g["seed"]))
+    x = torch.randn((B, 4, 32, 32)).to(cuda)
+    errs = {}
+    for i in range(1000, 0, -1):
+        t = torch.full((B,), i, dtype=torch.long, device=cuda)
+        x = d.denoise_cond(model16, x, t, y=y, guidance_scale=3.0, null_label=0, cond_vals=vals, cond_mask=mask)
+        if i in (900, 500, 100):
+            errs[i] = rel(x[:sub], g[f"x_{i}"])
+    errs[0] = rel(x, g["x_final"])
+    vae = VAE()
+    vae.load_state_dict(vae_sd)
+    vae = vae.to(cuda).eval()
+    n = int(g["u8"].shape[0])
+    u8 = vae.decode_uint8(x[:n].contiguous()).cpu().numpy().astype(np.int32)
+    du = np.abs(u8 - g["u8"].astype(np.int32))
+    print(f"[config4] T=1000 B=32 trajectory latent rel-L2 at t=900/500/100/final: "
+          + ", ".join(f"{errs[k]:.3e}" for k in (900, 500, 100, 0))
+          + f"; uint8 max|d| {du.max()}, differing {(du > 0).mean():.4f}")
+    for k, v in errs.items():
+        assert v < TOL_TRAJ, (k, v)
+    assert du.max() <= 2 and (du > 0).mean() <= 0.05
+
+
+def test_f16_forward_bench_batch_vs_oracle(model16, cuda, unet_sd):
+    """One 128-sample forward in fp16 mode (the config-4 bench batch: Winograd X1 instances at every
+    map size, 4 x 4 included) vs the fp32 oracle."""
+    g = torch.Generator().manual_seed(128)
+    N = 128
+    x = torch.randn((N, 4, 32, 32), generator=g)
+    t = torch.randint(1, 1001, (N,), generator=g)
+    y = torch.randint(0, 4, (N,), generator=g)
+    vals = torch.rand((N, 12), generator=g)
+    mask = (torch.rand((N, 12), generator=g) > 0.5).float()
+    with torch.no_grad():
+        eps, geom = model16(x.to(cuda), t.to(cuda), y.to(cuda), cond_vals=vals.to(cuda), cond_mask=mask.to(cuda))
+        e2, g2 = ref.unet_cond_geom_forward(unet_sd, x, t, y, vals, mask)
+    e, q = rel(eps, e2), rel(geom, g2)
+    print(f"[config4] forward N=128: eps rel-L2 {e:.3e}, geom rel-L2 {q:.3e}")
+    assert e < TOL_FWD and q < TOL_FWD
 
 
 def test_f16_vae_decode(golden, vae_sd, cuda):
