@@ -11,6 +11,58 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 namespace dmx {
 
 // ---------------------------------------------------------------------------
+// Whole-wave (64-lane) sums without the LDS pipe: DPP inside each 16-lane row (quad_perm [1,0,3,2],
+// [2,3,0,1], row_half_mirror, row_mirror), then v_permlane32_swap (rows 0+2, 1+3) and
+// v_permlane16_swap (the two pairs) — six VALU steps instead of six dependent ds_bpermute round
+// trips (__shfl_xor).  Fixed order; every lane gets the same bits.
+// ---------------------------------------------------------------------------
+template <int CTRL>
+DMX_DEV unsigned dpp_u32(unsigned v) {
+  return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+DMX_DEV float dpp_f32(float v) {
+  return __builtin_bit_cast(float, dpp_u32<CTRL>(__builtin_bit_cast(unsigned, v)));
+}
+template <int CTRL>
+DMX_DEV double dpp_f64(double v) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned long long lo = dpp_u32<CTRL>((unsigned)u), hi = dpp_u32<CTRL>((unsigned)(u >> 32));
+  return __builtin_bit_cast(double, lo | (hi << 32));
+}
+DMX_DEV float wave_sum_dpp(float s) {
+  s += dpp_f32<0xB1>(s);
+  s += dpp_f32<0x4E>(s);
+  s += dpp_f32<0x141>(s);
+  s += dpp_f32<0x140>(s);
+  unsigned u = __builtin_bit_cast(unsigned, s);
+  auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  s = __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+  u = __builtin_bit_cast(unsigned, s);
+  r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+DMX_DEV double wave_sum_dpp(double s) {
+  s += dpp_f64<0xB1>(s);
+  s += dpp_f64<0x4E>(s);
+  s += dpp_f64<0x141>(s);
+  s += dpp_f64<0x140>(s);
+  auto swap = [](double v, bool sixteen) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+    const auto a = sixteen ? __builtin_amdgcn_permlane16_swap(lo, lo, false, false)
+                           : __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto b = sixteen ? __builtin_amdgcn_permlane16_swap(hi, hi, false, false)
+                           : __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    const double x = __builtin_bit_cast(double, (unsigned long long)(unsigned)a[0] | ((unsigned long long)(unsigned)b[0] << 32));
+    const double y = __builtin_bit_cast(double, (unsigned long long)(unsigned)a[1] | ((unsigned long long)(unsigned)b[1] << 32));
+    return x + y;
+  };
+  s = swap(s, false);
+  return swap(s, true);
+}
+
+// ---------------------------------------------------------------------------
 // Exact (erf) GELU and SiLU in fp32, matching the reference's nn.GELU() /
 // F.gelu default (approximate='none') and nn.SiLU (models/unet_cond.py:21,28,63).
 // ---------------------------------------------------------------------------

@@ -46,7 +46,9 @@ namespace dmx {
 // Diagnostic builds only (-DDMX_WDIAG=bits; wrong results, timing decomposition): 1 no MFMAs,
 // 2 no A-fragment arithmetic (LDS reads kept), 4 no GroupNorm / GELU in the halo store, 8 no output
 // stores, 16 the output bytes stored as two contiguous float4 per thread (wrong layout), 32 no LDS
-// round trip in the epilogue (outputs from the wave's own accumulators).
+// round trip in the epilogue (outputs from the wave's own accumulators); chunk loop: 64 no barrier,
+// 128 no U reloads (chunk 0's fragments throughout), 256 no halo global loads, 512 no halo LDS
+// stores, 1024 no A-fragment LDS reads (halo values from registers).
 #ifndef DMX_WDIAG
 #define DMX_WDIAG 0
 #endif
@@ -56,6 +58,9 @@ namespace dmx {
 #endif
 #ifndef DMX_WBAR2  // (A/B build) a barrier between the halo store and the A build
 #define DMX_WBAR2 0
+#endif
+#ifndef DMX_WSHFL
+#define DMX_WSHFL 0
 #endif
 #ifndef DMX_WEPP
 #define DMX_WEPP 34
@@ -233,11 +238,8 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
           s1 += (double)q.x;
           s2 += (double)q.y;
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          s1 += __shfl_xor(s1, o, 64);
-          s2 += __shfl_xor(s2, o, 64);
-        }
+        s1 = wave_sum_dpp(s1);
+        s2 = wave_sum_dpp(s2);
         if ((tid & 63) == 0) {
           gr1[tid >> 6] = s1;
           gr2[tid >> 6] = s2;
@@ -258,6 +260,9 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   floatx4 ha[NPI];
   floatx4 hr[GNA == 2 ? NPI : 1];
   auto load_halo = [&](int c) {
+    if constexpr ((DMX_WDIAG & 256) != 0) {
+      if (c > 1) return;
+    }
 #pragma unroll
     for (int k = 0; k < NPI; ++k) {
       const int off = hoff[k] >= 0 ? (hoff[k] + (cbeg + c) * CK) * 4 : kOOB;
@@ -266,6 +271,9 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
     }
   };
   auto store_halo = [&](int buf, int c) {
+    if constexpr ((DMX_WDIAG & 512) != 0) {
+      if (c > 1) return;
+    }
     float* hb = lds + buf * HBUF;
     floatx4 ggam = {0.f, 0.f, 0.f, 0.f}, gbet = {0.f, 0.f, 0.f, 0.f};
     if constexpr (GNA) {  // every piece of this thread holds the same channel quad (512 % 4 == 0)
@@ -302,6 +310,9 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   half8 bh[2][2], bl[2][2];
   int cnext = 0;  // chunk whose fragments load_b(.., -1) fetches
   auto load_b = [&](int q, int n, int c) {
+    if constexpr ((DMX_WDIAG & 128) != 0) {
+      if (c < 0) return;
+    }
     const int cc = c < 0 ? cnext : c;
     bh[q][n] = bload_h8(rUh, voff, ub[q][n] + (cbeg + cc) * 1024);
     if constexpr (!X1) bl[q][n] = bload_h8(rUl, voff, ub[q][n] + (cbeg + cc) * 1024);
@@ -334,8 +345,14 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
       const int oc[3] = {op, oq, os};
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        const floatx4 da = *reinterpret_cast<const floatx4*>(hb + oa + oc[k] + 4 * h);
-        const floatx4 db = *reinterpret_cast<const floatx4*>(hb + ob + oc[k] + 4 * h);
+        floatx4 da, db;
+        if constexpr ((DMX_WDIAG & 1024) != 0) {
+          da = floatx4{hb[0], hb[1], (float)k, (float)h};
+          db = floatx4{hb[2], (float)oc[k], (float)k, (float)h};
+        } else {
+          da = *reinterpret_cast<const floatx4*>(hb + oa + oc[k] + 4 * h);
+          db = *reinterpret_cast<const floatx4*>(hb + ob + oc[k] + 4 * h);
+        }
         if constexpr (DMX_WDIAG & 2) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) T[k][e] = k == 2 ? db[e] : da[e];
@@ -459,7 +476,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
     build(c & 1, 1);
     cnext = min(c + 1, nch - 1);
     mfmas(1, true);
-    __syncthreads();
+    if constexpr ((DMX_WDIAG & 64) == 0) __syncthreads();
   }
 
   // ---- epilogue: Aᵀ M A per tile, four passes of 32 tiles x 32 channels through LDS
@@ -541,12 +558,17 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
         }
       }
       // partial of 4 tiles (16 pixels) x 32 channels = this wave's 64 lanes
-      if constexpr (EPI == EPI_STATS) {
+      if constexpr (EPI == EPI_STATS) {  // (DPP / permlane: no LDS round trips in the epilogue)
+#if DMX_WSHFL  // (A/B build: the ds_bpermute tree)
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
           s1 += __shfl_xor(s1, o, 64);
           s2 += __shfl_xor(s2, o, 64);
         }
+#else
+        s1 = wave_sum_dpp(s1);
+        s2 = wave_sum_dpp(s2);
+#endif
       }
       if (EPI == EPI_STATS && lane == 0) {  // the wave's 4 tiles: one tile row of one sample
         const int t = 32 * mb + 4 * wid, st = t / TPS, g = (tile0 + t - st * TPS) / 4;

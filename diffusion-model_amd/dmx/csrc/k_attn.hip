@@ -1,6 +1,8 @@
 // dmx — split-precision attention core instantiations (attention_x3_kernel, see launch.h).
 #include "launch.h"
 
+#include <cstdlib>
+
 namespace dmx {
 
 void launch_attention_x3(int D, int wpe, int x1, const float* qkv, float* out, int L, int C, dim3 grid,
@@ -33,7 +35,35 @@ static hipError_t go16(const float* qkv, float* out, int L, int C, int N, hipStr
   return hipSuccess;
 }
 
+// The 16 x 16 x 32 PV variant (attention16pv_kernel, default; DMX_ATT_PV16=0 selects attention16_kernel
+// for same-box A/B).
+template <int NW, int X1>
+static hipError_t go16pv(const float* qkv, float* out, int L, int C, int N, hipStream_t st) {
+  static size_t granted = 0;
+  const size_t bytes = att16pv_lds_bytes(L, X1);
+  if (bytes > granted) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&attention16pv_kernel<NW, X1>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e != hipSuccess) return e;
+    granted = bytes;
+  }
+  attention16pv_kernel<NW, X1><<<dim3(1, 4, N), NW * 64, bytes, st>>>(qkv, out, L, C);
+  return hipSuccess;
+}
+
+bool attention16_pv16() {
+  static const bool v = [] {
+    const char* e = std::getenv("DMX_ATT_PV16");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return v;
+}
+
 hipError_t launch_attention16(int nw, int x1, const float* qkv, float* out, int L, int C, int N, hipStream_t st) {
+  if (attention16_pv16()) {
+    if (nw == 16) return x1 ? go16pv<16, 1>(qkv, out, L, C, N, st) : go16pv<16, 0>(qkv, out, L, C, N, st);
+    return x1 ? go16pv<8, 1>(qkv, out, L, C, N, st) : go16pv<8, 0>(qkv, out, L, C, N, st);
+  }
   if (nw == 16) return x1 ? go16<16, 1>(qkv, out, L, C, N, st) : go16<16, 0>(qkv, out, L, C, N, st);
   return x1 ? go16<8, 1>(qkv, out, L, C, N, st) : go16<8, 0>(qkv, out, L, C, N, st);
 }
