@@ -35,8 +35,11 @@ static hipError_t go16(const float* qkv, float* out, int L, int C, int N, hipStr
   return hipSuccess;
 }
 
-// The 16 x 16 x 32 PV variant (attention16pv_kernel, default; DMX_ATT_PV16=0 selects attention16_kernel
-// for same-box A/B).
+// The 16 x 16 x 32 PV variant (attention16pv_kernel): measured in the eager breakdown (same box,
+// B = 64 CFG) 24.6 vs 26.7 us at L = 256 (sa5) but 175.1 vs 170.5 us at L = 1024 (sa6) — the core is
+// bound by its per-score VALU (exp, hi / lo split, max), which the variant's permlane swaps and fp32
+// denominator sums add to, not by the MFMAs it halves.  DMX_ATT_PV16: 2 (default) L <= 256 only,
+// 1 always, 0 never (same-box A/B).
 template <int NW, int X1>
 static hipError_t go16pv(const float* qkv, float* out, int L, int C, int N, hipStream_t st) {
   static size_t granted = 0;
@@ -51,16 +54,17 @@ static hipError_t go16pv(const float* qkv, float* out, int L, int C, int N, hipS
   return hipSuccess;
 }
 
-bool attention16_pv16() {
-  static const bool v = [] {
+static int attention16_pv16() {
+  static const int v = [] {
     const char* e = std::getenv("DMX_ATT_PV16");
-    return e == nullptr || std::atoi(e) != 0;
+    return e == nullptr ? 2 : std::atoi(e);
   }();
   return v;
 }
 
 hipError_t launch_attention16(int nw, int x1, const float* qkv, float* out, int L, int C, int N, hipStream_t st) {
-  if (attention16_pv16()) {
+  const int pv = attention16_pv16();
+  if (pv == 1 || (pv == 2 && L <= 256)) {
     if (nw == 16) return x1 ? go16pv<16, 1>(qkv, out, L, C, N, st) : go16pv<16, 0>(qkv, out, L, C, N, st);
     return x1 ? go16pv<8, 1>(qkv, out, L, C, N, st) : go16pv<8, 0>(qkv, out, L, C, N, st);
   }
