@@ -1585,6 +1585,17 @@ static bool tok_frag_enabled() {
   }();
   return v;
 }
+// DMX_TOK_WIDE (same-box A/B): 1 the C = 256 QKV runs tok_ln_qkv_w_kernel (8-wave blocks, 384 columns,
+// one round of blocks); 0 (default) the 4-wave 64-column tok_ln_qkv_kernel — the wide kernel measured
+// -0.2 % per CFG step (3 / 3 same-box rounds): fewer LayerNorm recomputes and blocks do not pay for
+// its one block per CU.
+static bool tok_qkv_wide() {
+  static const bool v = [] {
+    const char* e = std::getenv("DMX_TOK_WIDE");
+    return e != nullptr && std::atoi(e) != 0;
+  }();
+  return v;
+}
 static TokW tokw(const ConvW& c) {
   return TokW{c.Bh, c.Bl, c.bias, c.inv_scale, c.kpad, tok_frag_enabled() ? c.Fh : nullptr,
               tok_frag_enabled() ? c.Fl : nullptr};
@@ -1617,6 +1628,12 @@ static float* attn_block_fused(Run& R, const AttnW& a, const float* x, int N, in
                   std::to_string(x1) + ">",
               2.0 * M * C * 3.0 * C, 16.0 * (double)M * C);
       launch_tok_qkv_lds(C, tpb, x1, tp, gl, R.st);
+    } else if (tok_qkv_wide()) {
+      // C = 256: 8-wave blocks of 64 tokens x 384 columns (one round of blocks, LayerNorm twice per tile)
+      const dim3 grid(cdiv(M, 64), 2);
+      R.begin("tok_ln_qkv_w_kernel<" + cs + ", 384, 8, 4, " + std::to_string(x1) + ">", 2.0 * M * C * 3.0 * C,
+              16.0 * (double)M * C);
+      launch_tok_qkv_w(C, x1, tp, grid, R.st);
     } else {
       const int nb = 64;  // C = 256: 64 columns per block doubles the grid (M <= 8192 here)
       const dim3 grid(cdiv(M, 64), 3 * C / nb);

@@ -960,17 +960,25 @@ __global__ __launch_bounds__(NW * 64) void attention16pv_kernel(const float* qkv
 #pragma unroll
       for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sc[r]);
       mx = max_halves(mx);
-      if (c0 == 0 || mx > TAU) {
-        const float alpha = __builtin_amdgcn_exp2f(-mx);
+      // The reference moves per query (lane fr <-> query fr here), but O^T's lanes hold queries
+      // lane & 15 / 16 + (lane & 15): the per-query factors reach them by one v_permlane16_swap
+      // (rows 0 / 2 -> o0's lanes, rows 1 / 3 -> o1's), so the rescale runs wave-uniformly.
+      const bool mv = c0 == 0 || mx > TAU;
+      if (__builtin_amdgcn_ballot_w64(mv) != 0) {
+        const float ms = mv ? mx : 0.f;
+        const float alpha = mv ? __builtin_amdgcn_exp2f(-mx) : 1.f;
+        const unsigned ua = __builtin_bit_cast(unsigned, alpha);
+        const auto ra = __builtin_amdgcn_permlane16_swap(ua, ua, false, false);
+        const float a0 = __builtin_bit_cast(float, (unsigned)ra[0]), a1 = __builtin_bit_cast(float, (unsigned)ra[1]);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          o0[r] *= alpha;
-          o1[r] *= alpha;
+          o0[r] *= a0;
+          o1[r] *= a1;
         }
         lsum *= alpha;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sc[r] -= mx;
-        mref += mx;
+        for (int r = 0; r < 16; ++r) sc[r] -= ms;
+        mref += ms;
 #pragma unroll
         for (int r = 0; r < 16; ++r) negm[r] = -mref;
       }

@@ -38,8 +38,9 @@ static hipError_t go16(const float* qkv, float* out, int L, int C, int N, hipStr
 // The 16 x 16 x 32 PV variant (attention16pv_kernel): measured in the eager breakdown (same box,
 // B = 64 CFG) 24.6 vs 26.7 us at L = 256 (sa5) but 175.1 vs 170.5 us at L = 1024 (sa6) — the core is
 // bound by its per-score VALU (exp, hi / lo split, max), which the variant's permlane swaps and fp32
-// denominator sums add to, not by the MFMAs it halves.  DMX_ATT_PV16: 2 (default) L <= 256 only,
-// 1 always, 0 never (same-box A/B).
+// denominator sums add to, not by the MFMAs it halves; at L <= 256 only it is neutral in the whole
+// step (-0.1 %, 2 / 2 same-box rounds).  DMX_ATT_PV16: 0 (default) never, 2 L <= 256 only, 1 always
+// (same-box A/B; the stress-magnitude and golden tests pass with 1).
 template <int NW, int X1>
 static hipError_t go16pv(const float* qkv, float* out, int L, int C, int N, hipStream_t st) {
   static size_t granted = 0;
@@ -57,7 +58,7 @@ static hipError_t go16pv(const float* qkv, float* out, int L, int C, int N, hipS
 static int attention16_pv16() {
   static const int v = [] {
     const char* e = std::getenv("DMX_ATT_PV16");
-    return e == nullptr ? 2 : std::atoi(e);
+    return e == nullptr ? 0 : std::atoi(e);
   }();
   return v;
 }

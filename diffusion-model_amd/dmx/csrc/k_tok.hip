@@ -1,6 +1,8 @@
 // dmx — fused attention-block token kernel instantiations (tokmlp.h, see launch.h).
 #include "launch.h"
 
+#include <stdexcept>
+
 namespace dmx {
 
 void launch_tok_qkv_lds(int C, int tpb, int x1, const TokParams& tp, dim3 gl, hipStream_t st) {
@@ -33,6 +35,12 @@ void launch_tok_qkv(int C, int nb, int x1, const TokParams& tp, dim3 grid, hipSt
       break;
   }
 #undef TQ
+}
+
+void launch_tok_qkv_w(int C, int x1, const TokParams& tp, dim3 grid, hipStream_t st) {
+  if (C != 256) throw std::runtime_error("launch_tok_qkv_w: C = 256 only");
+  if (x1) tok_ln_qkv_w_kernel<256, 384, 8, 4, 1><<<grid, 512, 0, st>>>(tp);
+  else tok_ln_qkv_w_kernel<256, 384, 8, 4, 0><<<grid, 512, 0, st>>>(tp);
 }
 
 void launch_tok_out(int C, int tm, int x1, int nw, int lds, int tpb, const TokParams& tp, int blocks,

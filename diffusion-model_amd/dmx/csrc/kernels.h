@@ -320,11 +320,8 @@ static __global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
       s1 += (double)q.x;
       s2 += (double)q.y;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      s1 += __shfl_xor(s1, o, 64);
-      s2 += __shfl_xor(s2, o, 64);
-    }
+    s1 = wave_sum_dpp(s1);  // (DPP / permlane: no LDS round trips before the stores can start)
+    s2 = wave_sum_dpp(s2);
     if ((tid & 63) == 0) {
       r1[tid >> 6] = s1;
       r2[tid >> 6] = s2;
@@ -444,12 +441,7 @@ __global__ __launch_bounds__(1024) void reduce_norm_kernel(const float* partial,
   }
   __shared__ double r1[16], r2[16];
   __shared__ float2 st_s;
-  double d1 = s1, d2 = s2;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    d1 += __shfl_xor(d1, o, 64);
-    d2 += __shfl_xor(d2, o, 64);
-  }
+  const double d1 = wave_sum_dpp((double)s1), d2 = wave_sum_dpp((double)s2);
   if ((tid & 63) == 0) {
     r1[tid >> 6] = d1;
     r2[tid >> 6] = d2;

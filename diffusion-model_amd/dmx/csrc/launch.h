@@ -67,6 +67,8 @@ hipError_t launch_attention16(int nw, int x1, const float* qkv, float* out, int 
 void launch_attention_f32(int D, int qt, const float* qkv, float* out, int L, int C, dim3 grid, hipStream_t st);
 // fused attention-block token kernels (tokmlp.h), k_tok.hip.
 void launch_tok_qkv_lds(int C, int tpb, int x1, const TokParams& tp, dim3 grid, hipStream_t st);
+// C = 256 QKV with 8-wave blocks of 64 tokens x 384 columns (tok_ln_qkv_w_kernel); grid (M / 64, 2).
+void launch_tok_qkv_w(int C, int x1, const TokParams& tp, dim3 grid, hipStream_t st);
 void launch_tok_qkv(int C, int nb, int x1, const TokParams& tp, dim3 grid, hipStream_t st);
 void launch_tok_out(int C, int tm, int x1, int nw, int lds, int tpb, const TokParams& tp, int blocks,
                     hipStream_t st);

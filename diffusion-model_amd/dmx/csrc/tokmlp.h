@@ -177,9 +177,9 @@ DMX_DEV void tok_rows(const float* src, int ld, int m0, int M, const float* g, c
 // the GEMM's A operand exists (under the LayerNorm / epilogue phases and their barriers), so the
 // L2 round trip of the weights is off the critical path; tok_gemm_primed consumes them and keeps
 // PD steps in flight (rolling register prefetch).
-template <int C, int NT>
+template <int C, int NT, int PDM = DMX_TOK_PD>
 struct TokB {
-  static constexpr int S = C / 16, PD = S < DMX_TOK_PD ? S : DMX_TOK_PD;
+  static constexpr int S = C / 16, PD = S < PDM ? S : PDM;
   half8 h[PD][NT], l[PD][NT];
 };
 
@@ -208,19 +208,19 @@ DMX_DEV void tok_loadb(const TokBPtr& p, int s, half8* h, half8* l) {
     if constexpr (!X1) l[j] = *reinterpret_cast<const half8*>(p.wl + j * p.jstride + p.sstride * s);
   }
 }
-template <int C, int NT, int X1 = 0>
-DMX_DEV void tok_prime(const TokW& w, int nw, int fr, int fh, TokB<C, NT>& b) {
+template <int C, int NT, int X1 = 0, int PDM = DMX_TOK_PD>
+DMX_DEV void tok_prime(const TokW& w, int nw, int fr, int fh, TokB<C, NT, PDM>& b) {
   const TokBPtr p = tok_bptr(w, nw, fr, fh);
 #pragma unroll
-  for (int s = 0; s < TokB<C, NT>::PD; ++s) tok_loadb<NT, X1>(p, s, b.h[s], b.l[s]);
+  for (int s = 0; s < TokB<C, NT, PDM>::PD; ++s) tok_loadb<NT, X1>(p, s, b.h[s], b.l[s]);
 }
 
 // acc[j] = A[arow0 .. +32][0, C) . W[nw + 32j .. +32][0, C)^T  (x3 sum, still scaled by 2^e),
 // B fragments primed by tok_prime (same w, nw).
-template <int C, int NT, int X1 = 0>
+template <int C, int NT, int X1 = 0, int PDM = DMX_TOK_PD>
 DMX_DEV void tok_gemm_primed(const _Float16 (*Ah)[C + 8], const _Float16 (*Al)[C + 8], const TokW& w, int nw,
-                             TokB<C, NT>& b, floatx16 (&acc)[NT], int arow0, int fr, int fh) {
-  constexpr int S = C / 16, PD = TokB<C, NT>::PD;
+                             TokB<C, NT, PDM>& b, floatx16 (&acc)[NT], int arow0, int fr, int fh) {
+  constexpr int S = C / 16, PD = TokB<C, NT, PDM>::PD;
 #pragma unroll
   for (int j = 0; j < NT; ++j)
 #pragma unroll
@@ -278,6 +278,37 @@ __global__ __launch_bounds__(256) void tok_ln_qkv_kernel(const TokParams P) {
   __syncthreads();
   floatx16 acc[NT];
   tok_gemm_primed<C, NT, X1>(Ah, Al, P.w0, nw, b, acc, wm * 32, fr, fh);
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int col = nw + 32 * j + fr;
+    const float bias = P.w0.bias[col];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = m0 + wm * 32 + tok_r(fh, r);
+      if (m < P.M) P.out[(size_t)m * 3 * C + col] = acc[j][r] * P.w0.inv_scale + bias;
+    }
+  }
+}
+
+// TA for wide C (256): NW = 8 waves as 2 (32-token halves) x 4 (column quarters), 64 tokens x NB
+// of the 3C columns per block (grid.y = 3C / NB), each wave 32 x NB/4 (NT = NB / 128 tiles) with PD
+// k16 steps of B fragments in flight.  The LayerNorm of a token tile runs 3C / NB times instead of
+// 3C / 64 times (tok_ln_qkv_kernel<256, 64>: twelve), and the grid is one round of blocks.
+template <int C, int NB, int NW, int PD, int X1 = 0>
+__global__ __launch_bounds__(NW * 64) void tok_ln_qkv_w_kernel(const TokParams P) {
+  constexpr int WN = NW / 2, NT = NB / WN / 32;
+  static_assert(NT >= 1 && NB % (WN * 32) == 0, "tile");
+  __shared__ __attribute__((aligned(16))) _Float16 Ah[64][C + 8];
+  __shared__ __attribute__((aligned(16))) _Float16 Al[64][C + 8];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, fr = lane & 31, fh = lane >> 5;
+  const int wm = wid / WN, wn = wid % WN, m0 = blockIdx.x * 64;
+  const int nw = blockIdx.y * NB + wn * (NB / WN);
+  TokB<C, NT, PD> b;
+  tok_prime<C, NT, X1, PD>(P.w0, nw, fr, fh, b);  // weights in flight with the token loads
+  tok_rows<C, 64, ROWS_LN, NW>(P.x, C, m0, P.M, P.l1w, P.l1b, Ah, Al, nullptr, nullptr);
+  __syncthreads();
+  floatx16 acc[NT];
+  tok_gemm_primed<C, NT, X1, PD>(Ah, Al, P.w0, nw, b, acc, wm * 32, fr, fh);
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     const int col = nw + 32 * j + fr;
