@@ -175,6 +175,23 @@ def legs(nm, model, x, y, vals, mask, args, tables, seed):
                          "ms_per_step": round(dt / k * 1e3, 4), "steps": k,
                          "path": "Diffuser.sample_latent_cond loop: eager dmx_step per step, noise from torch's CPU "
                                  "generator in the reference's draw order (helper-thread draws, pinned async H2D)"}
+    # the reference sampler's own latent shape (diff.py:315-322: the 224 dummy through VAE.encode gives
+    # 28 x 28 x 4), same batch and loop (graph replay, device noise)
+    x28, y28, v28, m28 = make_inputs(args.batch, 28, x.device, seed=7)
+    t_dev = torch.full((1,), args.T, dtype=torch.long, device=x.device)
+    nm.sample_loop(x28, t_dev, y28, 0, v28, m28, args.guidance, tables, 3, seed=seed)
+    torch.cuda.synchronize()
+    t_dev.fill_(args.T)
+    t0 = time.perf_counter()
+    nm.sample_loop(x28, t_dev, y28, 0, v28, m28, args.guidance, tables, k, seed=seed)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    assert torch.isfinite(x28).all(), "non-finite latents (28x28 leg)"
+    out["latent28"] = {"value": round(k / dt, 3), "unit": "CFG batch-steps/s (B=%d, 28x28x4)" % args.batch,
+                       "ms_per_step": round(dt / k * 1e3, 4), "steps": k,
+                       "pixel_rate_vs_32": None,  # filled in by main() (per-latent-pixel rate ratio)
+                       "note": "reference default sampler shape (diff.py:315-322); the 28 / 14 / 7 maps run the "
+                               "direct halo / implicit-GEMM convs (Winograd tiles cover 32 / 16 / 8 / 4 maps)"}
     return out
 
 
@@ -681,6 +698,8 @@ def main():
         out["config5"] = config5(nm, args, tables, seed)
     if world == 1 and args.legs_steps > 0:
         out.update(legs(nm, model, x, y, vals, mask, args, tables, seed))
+        if "latent28" in out:
+            out["latent28"]["pixel_rate_vs_32"] = round(out["latent28"]["value"] * 28 * 28 / (value * 32 * 32), 3)
     if world == 1 and args.e2e:
         out["e2e"] = e2e_sample(model, args, dev)
     if args.sharded_T > 0:

@@ -412,6 +412,12 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   if constexpr (RING0) __syncthreads();
   store_halo(0, 0);
   load_halo(min(1, nch - 1));
+  // Pin the issue order (chunk 1's halo loads older than chunk 0's U loads, as in the loop body): the
+  // scheduler otherwise hoisted four U loads above them, and the vmcnt wait the compiler derives at
+  // the loop head (merged over this entry and the back edge) then also drained two U loads of the
+  // previous chunk before every halo store — the U latency landed in front of the store and the A
+  // build instead of under them.
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int q = 0; q < 2; ++q)
 #pragma unroll
