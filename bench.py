@@ -190,8 +190,8 @@ def legs(nm, model, x, y, vals, mask, args, tables, seed):
     out["latent28"] = {"value": round(k / dt, 3), "unit": "CFG batch-steps/s (B=%d, 28x28x4)" % args.batch,
                        "ms_per_step": round(dt / k * 1e3, 4), "steps": k,
                        "pixel_rate_vs_32": None,  # filled in by main() (per-latent-pixel rate ratio)
-                       "note": "reference default sampler shape (diff.py:315-322); the 28 / 14 / 7 maps run the "
-                               "direct halo / implicit-GEMM convs (Winograd tiles cover 32 / 16 / 8 / 4 maps)"}
+                       "note": "reference default sampler shape (diff.py:315-322); the 28 / 14 / 7 / 3 maps run the "
+                               "Winograd convs in their 32 / 16 / 8 / 4 geometries (zero-padded columns)"}
     return out
 
 

@@ -1013,17 +1013,29 @@ static int wino_mask() {
 // batch) when the batch has >= 64 samples, of 2 samples below that (single-sample and small batches
 // keep a full grid).  A batch and its shards in the same class sum every output in the same order
 // (bit-identical results: test_gpu_poison.py's B = 5 vs 3 + 2; a 64-per-rank shard plans as the bench).
+// Winograd geometry of an H x W map (igemm_wino.h): the block width 32 / 16 / 8 / 4 the map fits —
+// 8-row bands of any height at 32, whole samples (H <= width) below; 0 = none.  The reference's 28 x 28
+// latents (diff.py:315-322) run their 28 / 14 / 7 / 3 maps in the 32 / 16 / 8 / 4 geometries.
+static int wino_geom(int H, int W) {
+  if (W > 16 && W <= 32) return 32;
+  const int g = W > 8 ? 16 : W > 4 ? 8 : W >= 2 ? 4 : 0;
+  return (g != 0 && H <= g) ? g : 0;
+}
+static int wino_blocks(int G, int N, int H) {  // blocks along the pixel axis
+  return G == 32 ? N * cdiv(H, 8) : cdiv(N, G == 8 ? 4 : G == 4 ? 16 : 1);
+}
 static int wino_plan(const Run& R, int src_C, int N, int H, int W, const ConvW& cw, int* cps) {
   // (U-Net only: the VAE decoder keeps its per-sample-tiled direct convs, Run::tile_n)
   if (!wino_enabled() || R.m->prec < 1 || (R.m->prec == 2 && !wino_f16_enabled()) || R.m->kind == DMX_VAE ||
       R.tile_n > 0 || cw.Uh == nullptr ||
       cw.phases != 1 || cw.taps != 9)
     return 0;
-  if (!((W == 32 && H % 8 == 0) || (W == 16 && H == 16) || (W == 8 && H == 8) || (W == 4 && H == 4))) return 0;
-  if (!((wino_mask() >> (W == 8 ? 0 : W == 16 ? 1 : W == 32 ? 2 : 3)) & 1)) return 0;
+  const int G = wino_geom(H, W);
+  if (G == 0) return 0;
+  if (!((wino_mask() >> (G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3)) & 1)) return 0;
   if (src_C % 16 != 0 || cw.cout % 64 != 0 || (size_t)16 * cw.cout * src_C * 2 >= ((size_t)1 << 31)) return 0;
   const int nref = dec_n(R, N) >= 64 ? 128 : 2;
-  const int blocks = cdiv(nref * H * W, 256) * (cw.cout / 64), nch = src_C / 16;
+  const int blocks = wino_blocks(G, nref, H) * (cw.cout / 64), nch = src_C / 16;
   int sp = 1, cp = nch;
   if (blocks < 256) {
     // (small-batch class: the split Winograd conv lost to the direct kernels — config 5, B = 1 CFG:
@@ -1033,7 +1045,7 @@ static int wino_plan(const Run& R, int src_C, int N, int H, int W, const ConvW& 
     cp = cdiv(nch, sp);
     sp = cdiv(nch, cp);
   }
-  if (W == 4 && sp == 1) return 0;  // (4 x 4: split-K instances only; sixteen samples per block)
+  if (G == 4 && sp == 1) return 0;  // (4 x 4: split-K instances only; sixteen samples per block)
   if (cps != nullptr) *cps = cp;
   return sp;
 }
@@ -1158,7 +1170,10 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   }
   float* partial = splits > 1 ? R.ws.get<float>((size_t)splits * M * cw.cout) : nullptr;
   const int rgrp = (splits == 1 && (H * W) % 32 == 0) ? 32 : 1;
-  const int rrows = (wino && splits == 1) ? H * W / 16 : cw.phases * H * W / rgrp;  // GroupNorm partial rows / sample
+  const int wg = wino ? wino_geom(H, W) : 0;
+  // GroupNorm partial rows / sample (Winograd: one per 4 tiles of the geometry, igemm_wino.h)
+  const int rrows = (wino && splits == 1) ? wino_blocks(wg, 1, H) * 64 / (wg == 8 ? 4 : wg == 4 ? 16 : 1) / 4
+                                          : cw.phases * H * W / rgrp;
   if (defer != nullptr) {
     defer->fused = splits > 1 && epi == EPI_STATS && !R.m->debug && rn_fuse_enabled() &&
                    H * W * (cw.cout / 4) <= RN_MAXV * 1024;  // (debug taps read the raw conv output)
@@ -1301,10 +1316,10 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
       check_range(R, cw.Uh, xp.u_bytes, "U hi");
       check_range(R, cw.Ul, xp.u_bytes, "U lo");
       const int e = splits > 1 ? (int)EPI_PARTIAL : (int)EPI_STATS;
-      if (x1) std::snprintf(nm, sizeof nm, "wino_kernel<%d, %d, %d, 1>", W, gna, e);
-      else std::snprintf(nm, sizeof nm, "wino_kernel<%d, %d, %d>", W, gna, e);
+      if (x1) std::snprintf(nm, sizeof nm, "wino_kernel<%d, %d, %d, 1>", wg, gna, e);
+      else std::snprintf(nm, sizeof nm, "wino_kernel<%d, %d, %d>", wg, gna, e);
       R.begin(nm, flops, bytes + (splits > 1 ? 4.0 * splits * M * cw.cout : 0.0));
-      launch_wino(e, W, gna, x1 ? 1 : 0, xp, dim3(cdiv(M, 256), cw.cout / 64, splits), R.st);
+      launch_wino(e, wg, gna, x1 ? 1 : 0, xp, dim3(wino_blocks(wg, N, H), cw.cout / 64, splits), R.st);
       R.end();
       HIPCHK(hipGetLastError());
       if (splits == 1 || (defer != nullptr && defer->fused)) return rrows;

@@ -34,7 +34,9 @@
 // Epilogue: in four passes of (32 tiles x 32 channels) the 16 position accumulators go through LDS,
 // every thread applies Aᵀ M A to two tiles of one channel in a fixed order, stores the 2x2 pixels
 // (NHWC fp32) and the GroupNorm (sum, sum of squares) partials of 16-pixel x 32-channel groups
-// (HW / 16 partial rows per sample: the caller's consumers reduce a sample's partials in any layout).
+// (one partial row per 4 geometry tiles: the caller's consumers reduce a sample's partials in any layout).
+// Maps narrower than the geometry (the reference's 28 x 28 latents: 28 / 14 / 7 / 3 maps in the 32 / 16
+// / 8 / 4 geometries) run the same blocks with the missing columns and rows as zero padding.
 #pragma once
 #include "common.h"
 #include "igemm.h"
@@ -196,10 +198,16 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   const int wi = wid >> 1, jp = wid & 1;
   int mt, nt, bz;
   xcd_tile(mt, nt, bz);
-  const int m0 = mt * 256;
-  const int HW = p.H * W, C = p.src.C;
-  const int nsmp = m0 / HW, y0 = (m0 - nsmp * HW) / W;  // first sample of the block; W = 32: first row
-  const int nsamp = p.M / HW;  // W = 8: samples past the batch (last block) stage zeros, write nothing
+  // The map is p.H x p.W (WA) inside the W-wide geometry: WA <= W columns (W = 32: any height, 8-row
+  // bands, BPS per sample; W <= 16: p.H <= W, whole samples).  Halo pixels past the map stage zeros
+  // (the conv's zero padding), outputs past it are neither stored nor counted in the partials.
+  const int WA = p.W;
+  const int BPS = W == 32 ? (p.H + 7) >> 3 : 1;  // blocks per sample
+  const int HW = p.H * WA, C = p.src.C;
+  const int nsmp = W == 32 ? mt / BPS : mt * SPB;  // first sample of the block
+  const int band = W == 32 ? mt - nsmp * BPS : 0;
+  const int y0 = 8 * band;  // W = 32: first row of the band
+  const int nsamp = p.M / HW;  // W = 8 / 4: samples past the batch (last block) stage zeros, write nothing
   const int nch_all = C / CK;
   const int cbeg = EPI == EPI_PARTIAL ? bz * p.ksplit : 0;  // first chunk of this split
   const int nch = EPI == EPI_PARTIAL ? min(p.ksplit, nch_all - cbeg) : nch_all;
@@ -216,8 +224,8 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
     const int ry = RING0 ? ((h >> 2) & 3) + 1 : h / HC - sh * PS;
     const int hx = RING0 ? (h & 3) + 1 : h - (h / HC) * HC;
     const int y = y0 + ry - 1, x = hx - 1;
-    const bool ok = e < NPC && ry < HRS && y >= 0 && y < p.H && x >= 0 && x < W && nsmp + sh < nsamp;
-    hoff[k] = ok ? ((((nsmp + sh) * p.H + y) * W + x) * C + q * 4) : -1;
+    const bool ok = e < NPC && ry < HRS && y >= 0 && y < p.H && x >= 0 && x < WA && nsmp + sh < nsamp;
+    hoff[k] = ok ? ((((nsmp + sh) * p.H + y) * WA + x) * C + q * 4) : -1;
     // pieces past the halo store to a scratch slot of their own (no divergent branch around the store)
     hls[k] = e < NPC ? (sh * SQ + (ry * 2 + (hx & 1)) * RP * 4 + (hx >> 1) * 20 + q * 4) : 2 * HBUF + (tid & 255) * 4;
   }
@@ -488,8 +496,9 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   // ---- epilogue: Aᵀ M A per tile, four passes of 32 tiles x 32 channels through LDS
   __syncthreads();  // (the halo buffers become the epilogue's staging area)
   WSTAMP(2);
-  const int HW16 = HW / 16, nseg = p.Cout / 32;
-  const int tile0 = (m0 - nsmp * HW) / 4;  // first tile of the block inside its sample
+  // GroupNorm partial rows per sample: one per 4 geometry tiles (rows wholly past the map hold zeros)
+  const int HW16 = BPS * 64 / SPB / 4, nseg = p.Cout / 32;
+  const int tile0 = band * 64;  // first tile of the block inside its sample
   const int cc = tid & 31, tp = tid >> 5;  // output task: channel cc, tiles 2 tp, 2 tp + 1
 #pragma unroll
   for (int mb = 0; mb < 2; ++mb)
@@ -545,14 +554,16 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
           for (int s = 0; s < 2; ++s) {
             const float y = (r == 0 ? (z[0][s] + z[1][s]) + z[2][s] : (z[1][s] - z[2][s]) - z[3][s]) + bias;
             const int oy = y0 + 2 * ty + r, ox = 2 * tx + s;
-            if (!(DMX_WDIAG & 24) && nsmp + st < nsamp) {
-              float* a = &dst[(((size_t)(nsmp + st) * p.H + oy) * W + ox) * p.Cout + col];
+            const bool in = oy < p.H && ox < WA;
+            if (!(DMX_WDIAG & 24) && nsmp + st < nsamp && in) {
+              float* a = &dst[(((size_t)(nsmp + st) * p.H + oy) * WA + ox) * p.Cout + col];
               if constexpr (DMX_WNT && (EPI == EPI_STATS || DMX_WNT_PART)) __builtin_nontemporal_store(y, a);
               else *a = y;
             }
             ys[4 * e + 2 * r + s] = y;
-            s1 += y;
-            s2 += y * y;
+            const float yv = in ? y : 0.f;
+            s1 += yv;
+            s2 += yv * yv;
           }
       }
       if constexpr ((DMX_WDIAG & 16) != 0) {  // same bytes as two contiguous float4 per thread (wrong layout)

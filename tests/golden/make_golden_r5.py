@@ -1,6 +1,6 @@
 """Round-5 golden vector: a T=1000 CFG trajectory at the Winograd batch class.
 
-Run from the repo root:  python tests/golden/make_golden_r5.py
+Run from the repo root:  python tests/golden/make_golden_r5.py [28]
 Same rules as make_golden.py: the reference is imported read-only from /root/reference
 (one harness-side ``torchvision.transforms.ToPILImage`` stub), only the fixture written
 here travels to the GPU box.
@@ -13,6 +13,11 @@ CFG 3.0 — a 64-sample CFG forward per step, i.e. the batch class (>= 64 sample
 after t = 900, 500, 100 for samples 0..7 (samples evolve independently, so a subset pins
 the intermediate states); the reference's VAE.decode -> reverse_to_img uint8 images of
 samples 0..5.
+
+traj_T1000_B32_28.npz (argument 28) — the same at 28x28x4 latents, the shape the reference's own
+sampler draws (diff.py:315-322 with the 224 encode dummy): the 28 / 14 / 7 / 3 maps whose 3x3 convs
+dmx runs in the Winograd kernel's 32 / 16 / 8 / 4 geometries with the missing rows / columns as
+zero padding (seed 51).
 """
 from __future__ import annotations
 
@@ -34,6 +39,9 @@ CKPTS = (900, 500, 100)
 
 
 def main():
+    hw = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+    seed = SEED if hw == 32 else SEED + 1
+    name = "traj_T1000_B32.npz" if hw == 32 else f"traj_T1000_B32_{hw}.npz"
     torch.set_num_threads(int(os.environ.get("GOLDEN_THREADS", "8")))
     _install_torchvision_stub()
     sys.path.insert(0, os.path.join(REPO, "diffusion-model_amd"))
@@ -53,11 +61,11 @@ def main():
     d = rdiff.Diffuser(num_timesteps=T, device="cpu")
 
     y = torch.tensor([1 + i % 3 for i in range(B)], dtype=torch.long)
-    g = torch.Generator().manual_seed(SEED - 1)
+    g = torch.Generator().manual_seed(seed - 1)
     vals = torch.rand((B, 12), generator=g)
     mask = (torch.rand((B, 12), generator=g) > 0.3).float()
-    torch.manual_seed(SEED)
-    x = torch.randn((B, 4, 32, 32))
+    torch.manual_seed(seed)
+    x = torch.randn((B, 4, hw, hw))
     ck = {}
     with torch.no_grad():
         for i in range(T, 0, -1):
@@ -69,7 +77,7 @@ def main():
                 print(f"[golden-r5] t={i} {time.time() - t0:.0f}s", flush=True)
         img = vae.decode(x[:IMGS])
     u8 = np.stack([np.asarray(d.reverse_to_img(img[i])) for i in range(IMGS)])
-    np.savez_compressed(os.path.join(HERE, "traj_T1000_B32.npz"), seed=SEED, y=y.numpy(), vals=vals.numpy(),
+    np.savez_compressed(os.path.join(HERE, name), seed=seed, y=y.numpy(), vals=vals.numpy(),
                         mask=mask.numpy(), x_final=x.numpy(), u8=u8, sub=SUB, **ck)
     print(f"[golden-r5] done {time.time() - t0:.0f}s", flush=True)
 

@@ -144,12 +144,13 @@ def test_f16_trajectory_T1000_B32_winograd_class(golden, model16, vae_sd, cuda):
     assert du.max() <= 2 and (du > 0).mean() <= 0.05
 
 
-def test_f16_forward_bench_batch_vs_oracle(model16, cuda, unet_sd):
+@pytest.mark.parametrize("hw", [32, 28])
+def test_f16_forward_bench_batch_vs_oracle(model16, cuda, unet_sd, hw):
     """One 128-sample forward in fp16 mode (the config-4 bench batch: Winograd X1 instances at every
-    map size, 4 x 4 included) vs the fp32 oracle."""
-    g = torch.Generator().manual_seed(128)
+    map size, 4 x 4 included; 28x28: the narrower maps in the same geometries) vs the fp32 oracle."""
+    g = torch.Generator().manual_seed(128 + hw)
     N = 128
-    x = torch.randn((N, 4, 32, 32), generator=g)
+    x = torch.randn((N, 4, hw, hw), generator=g)
     t = torch.randint(1, 1001, (N,), generator=g)
     y = torch.randint(0, 4, (N,), generator=g)
     vals = torch.rand((N, 12), generator=g)
@@ -158,7 +159,7 @@ def test_f16_forward_bench_batch_vs_oracle(model16, cuda, unet_sd):
         eps, geom = model16(x.to(cuda), t.to(cuda), y.to(cuda), cond_vals=vals.to(cuda), cond_mask=mask.to(cuda))
         e2, g2 = ref.unet_cond_geom_forward(unet_sd, x, t, y, vals, mask)
     e, q = rel(eps, e2), rel(geom, g2)
-    print(f"[config4] forward N=128: eps rel-L2 {e:.3e}, geom rel-L2 {q:.3e}")
+    print(f"[config4] forward N=128 {hw}x{hw}: eps rel-L2 {e:.3e}, geom rel-L2 {q:.3e}")
     assert e < TOL_FWD and q < TOL_FWD
 
 

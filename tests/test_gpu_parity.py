@@ -84,13 +84,16 @@ def test_unet_forward_vs_oracle_no_cond(model, cuda, unet_sd):
     assert rel(eps, e2) < TOL and rel(geom, g2) < TOL
 
 
-def test_unet_forward_bench_batch_vs_oracle(model, cuda, unet_sd, prec):
+@pytest.mark.parametrize("hw", [32, 28])
+def test_unet_forward_bench_batch_vs_oracle(model, cuda, unet_sd, prec, hw):
     """One forward of 128 samples (the CFG batch of B=64): the batch at which the 16x16 / 32x32 convs
     take their large-grid kernels — in x3 mode the Winograd F(2x2, 3x3) convs (igemm_wino.h) — checked
-    on eps itself (a CFG step's latent hides eps errors behind its (1-a)/sqrt(1-ab) factor)."""
-    g = torch.Generator().manual_seed(128)
+    on eps itself (a CFG step's latent hides eps errors behind its (1-a)/sqrt(1-ab) factor).  28x28:
+    the 28 / 14 / 7 / 3 maps in the Winograd geometries of 32 / 16 / 8 / 4 (zero-padded rows and
+    columns, partial GroupNorm rows) and the Up path's pad."""
+    g = torch.Generator().manual_seed(128 + hw)
     N = 128
-    x = torch.randn((N, 4, 32, 32), generator=g)
+    x = torch.randn((N, 4, hw, hw), generator=g)
     t = torch.randint(1, 1001, (N,), generator=g)
     y = torch.randint(0, 4, (N,), generator=g)
     vals = torch.rand((N, 12), generator=g)
@@ -99,7 +102,7 @@ def test_unet_forward_bench_batch_vs_oracle(model, cuda, unet_sd, prec):
         eps, geom = model(x.to(cuda), t.to(cuda), y.to(cuda), cond_vals=vals.to(cuda), cond_mask=mask.to(cuda))
         e2, g2 = ref.unet_cond_geom_forward(unet_sd, x, t, y, vals, mask)
     ee, eg = rel(eps, e2), rel(geom, g2)
-    print(f"[forward N=128 {prec}] eps rel-L2 {ee:.2e}, geom {eg:.2e}")
+    print(f"[forward N=128 {hw}x{hw} {prec}] eps rel-L2 {ee:.2e}, geom {eg:.2e}")
     assert ee < TOL and eg < TOL
 
 
@@ -308,14 +311,15 @@ def test_cfg_step_full_batch_vs_oracle(model, cuda, unet_sd, prec):
     assert rel(out, exp) < TOL
 
 
-@pytest.mark.parametrize("B,hw", [(3, 32), (9, 32), (5, 16), (33, 32)])
+@pytest.mark.parametrize("B,hw", [(3, 32), (9, 32), (5, 16), (33, 32), (33, 28)])
 def test_cfg_step_ragged_batches_vs_oracle(model, cuda, unet_sd, B, hw):
     """Batches that are not a multiple of the low-resolution halo convs' whole-sample tiles (16
     samples of 4 x 4, 4 of 8 x 8: igemm_halo.h MS) — the last tile holds fewer samples, which stage
     as zeros and whose rows the epilogue drops — and the split-K slab reduction behind them.
     B = 33 (a 66-sample CFG forward) is in the benchmark's batch class (>= 64 samples): its 3x3 convs
     run the Winograd kernels, whose 8 x 8 blocks stack four samples, so the last block holds 2
-    (igemm_wino.h nsamp guards)."""
+    (igemm_wino.h nsamp guards).  B = 33 at 28x28: the same with the maps narrower
+    than the Winograd geometries (7 x 7 in the 8-wide blocks, 3 x 3 in the 4-wide ones)."""
     import diff
     d = diff.Diffuser(1000, device=cuda)
     g = torch.Generator().manual_seed(300 + B)
@@ -359,14 +363,16 @@ def test_trajectory_T1000_golden(golden, model, vae, cuda, prec):
     assert ok, info
 
 
-def test_trajectory_T1000_B32_winograd_class_golden(golden, model, vae, cuda):
+@pytest.mark.parametrize("name", ["traj_T1000_B32.npz", "traj_T1000_B32_28.npz"])
+def test_trajectory_T1000_B32_winograd_class_golden(golden, model, vae, cuda, name):
     """T=1000 CFG trajectory at B=32 (a 64-sample CFG forward: the batch class whose 3x3 convs run the
     Winograd kernels bench.py times) on the reference's own draws (tests/golden/make_golden_r5.py,
     diff.py:326-344 loop of denoise_cond): latents at t = 900 / 500 / 100 (samples 0..7) and after
     t = 1 (all 32) within 1e-4 rel-L2, decoded uint8 images of samples 0..5 within +-1 LSB on <= 0.1 %.
-    x3 mode (the default, fp32 semantics)."""
+    x3 mode (the default, fp32 semantics).  traj_T1000_B32_28.npz: the same at
+    28x28 latents (the reference sampler's shape; Winograd geometries with zero-padded columns)."""
     import diff
-    g = golden("traj_T1000_B32.npz")
+    g = golden(name)
     nm = model.native()
     assert nm.precision == "x3"
     B, sub = int(g["y"].shape[0]), int(g["sub"])
@@ -374,7 +380,8 @@ def test_trajectory_T1000_B32_winograd_class_golden(golden, model, vae, cuda):
     y = torch.from_numpy(g["y"]).to(cuda)
     vals, mask = torch.from_numpy(g["vals"]).to(cuda), torch.from_numpy(g["mask"]).to(cuda)
     torch.manual_seed(int(g["seed"]))
-    x = torch.randn((B, 4, 32, 32)).to(cuda)
+    hw = int(g["x_final"].shape[-1])
+    x = torch.randn((B, 4, hw, hw)).to(cuda)
     errs = {}
     for i in range(1000, 0, -1):
         t = torch.full((B,), i, dtype=torch.long, device=cuda)
@@ -385,7 +392,7 @@ def test_trajectory_T1000_B32_winograd_class_golden(golden, model, vae, cuda):
     n_img = int(g["u8"].shape[0])
     u8 = vae.decode_uint8(x[:n_img].contiguous()).cpu().numpy()
     ok, info = u8_close(u8, g["u8"])
-    print(f"[trajectory T=1000 B=32 x3] latents rel-L2 vs reference {errs}, pixels {info}")
+    print(f"[trajectory T=1000 B=32 {hw}x{hw} x3] latents rel-L2 vs reference {errs}, pixels {info}")
     assert all(e < 1e-4 for e in errs.values()), errs
     assert ok, info
 
