@@ -1103,17 +1103,19 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   const int M = N * H * W;
   const int Md = dec_n(R, N) * H * W;  // rows the decisions below are taken for
   if (cw.cout % 32 != 0) throw Error(DMX_E_INTERNAL, "gemm: Cout must be a multiple of 32");
+  const int cin_px = W % 32 == 0 ? 32 : (W >= 16 && W <= 32 && (H * W) % 16 == 0) ? 16 : 0;  // conv_in_kernel<PX>
   if (src_mode == SRC_NCHW && epi == EPI_STATS && cw.taps == 9 && cw.phases == 1 && cw.cin == 4 && cw.cout == 64 &&
-      W % 32 == 0 && seg == 32 && cw.bias == nullptr && R.m->kind != DMX_VAE && gn == nullptr) {
-    // inc's first conv: direct fp32 conv of the NCHW input (kernels.h conv_in_kernel)
+      cin_px > 0 && seg == 32 && cw.bias == nullptr && R.m->kind != DMX_VAE && gn == nullptr) {
+    // inc's first conv: direct fp32 conv of the NCHW input (kernels.h conv_in_kernel; 16-pixel blocks for
+    // the 28-wide latents)
     if (res != nullptr) throw Error(DMX_E_INTERNAL, "gemm: the direct input conv takes no residual");
     if (ash != nullptr || asl != nullptr) throw Error(DMX_E_INTERNAL, "gemm: the direct input conv reads fp32 NCHW");
     if (defer != nullptr) *defer = Deferred{};  // whole K, no slabs
-    if (R.plan) return H * W / 32;
+    if (R.plan) return H * W / cin_px;
     if (check_args()) {  // (as every other GEMM path; the NCHW input is the caller's tensor, not checked)
       check_range(R, cw.B, (size_t)cw.phases * cw.npad * cw.kpad * 4, "B");
       check_range(R, out, (size_t)M * 64 * 4, "out");
-      check_range(R, rowpart, (size_t)N * (H * W / 32) * (64 / 32) * sizeof(float2), "rowpart");
+      check_range(R, rowpart, (size_t)N * (H * W / cin_px) * (64 / 32) * sizeof(float2), "rowpart");
     }
     ConvInParams q;
     q.x = s.src0;
@@ -1127,11 +1129,13 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
     q.rowpart = rowpart;
     q.H = H;
     q.W = W;
-    R.begin("conv_in_kernel", 2.0 * M * 64.0 * 9.0 * q.creal, 4.0 * ((double)M * 64 + (double)M * q.creal));
-    conv_in_kernel<<<M / 32, 256, 0, R.st>>>(q);
+    R.begin(cin_px == 32 ? "conv_in_kernel<32>" : "conv_in_kernel<16>", 2.0 * M * 64.0 * 9.0 * q.creal,
+            4.0 * ((double)M * 64 + (double)M * q.creal));
+    if (cin_px == 32) conv_in_kernel<32><<<M / 32, 256, 0, R.st>>>(q);
+    else conv_in_kernel<16><<<M / 16, 256, 0, R.st>>>(q);
     R.end();
     HIPCHK(hipGetLastError());
-    return H * W / 32;
+    return H * W / cin_px;
   }
   const int bn = (cw.cout % 128 == 0) ? 128 : 64;
   const int tiles128 = cdiv(Md, 128) * cdiv(cw.cout, bn) * cw.phases;

@@ -130,11 +130,12 @@ static __global__ __launch_bounds__(256) void embed_kernel(const EmbedParams p) 
 // inc's first conv (models/unet_cond.py:17, Conv2d(in_ch, 64, 3, padding=1, bias=False)) on the NCHW
 // network input: K = 9 taps x <= 4 channels is far too thin for a GEMM (the implicit GEMM padded it
 // to 64 and paid a global round trip per 16-deep K step), so it runs as a direct fp32 conv: a block
-// owns 32 output pixels (one image row segment, W % 32 == 0) x 64 channels, each output accumulates
-// its 36 products in fixed (tap, channel) order with fp32 FMAs (exact fp32
-// semantics in every precision mode).  Output NHWC fp32 plus the
-// GroupNorm (sum, sum of squares) partial of each (32 pixels, 32 channels) group — the layout
-// igemm_epilogue writes (rgrp = 32, seg = 32).
+// owns PX consecutive output pixels of one sample x 64 channels — PX = 32: one image row segment
+// (W % 32 == 0); PX = 16: any 16 pixels of a map 16..32 wide (H W % 16 == 0: the reference sampler's
+// 28 x 28 latents), spanning at most two image rows — each output accumulates its 36 products in
+// fixed (tap, channel) order with fp32 FMAs (exact fp32 semantics in every precision mode).  Output
+// NHWC fp32 plus the GroupNorm (sum, sum of squares) partial of each (PX pixels, 32 channels) group —
+// the layout igemm_epilogue writes (rgrp = PX, seg = 32).
 // ---------------------------------------------------------------------------
 struct ConvInParams {
   const float* x;      // NCHW [n][creal][H][W]
@@ -143,15 +144,19 @@ struct ConvInParams {
   const float* B;      // packed [npad][kpad], k = tap * cin + c
   int cin, kpad;
   float* out;          // NHWC [n][H][W][64]
-  float2* rowpart;     // [n][HW / 32][2]
+  float2* rowpart;     // [n][HW / PX][2]
   int H, W;
 };
-static __global__ __launch_bounds__(256) void conv_in_kernel(const ConvInParams p) {
-  // thread (output channel co, pixel group pg): pixels 8 pg .. 8 pg + 7 of the block's 32; its 36
-  // weights in registers, the 3 x 34 x 4 input patch in LDS (float4 per pixel: one broadcast
-  // ds_read_b128 per pixel and tap), one coalesced 256-byte row of channels per pixel store
+template <int PX>
+__global__ __launch_bounds__(256) void conv_in_kernel(const ConvInParams p) {
+  // thread (output channel co, pixel group pg): pixels PX / 4 pg .. + PX / 4 - 1 of the block's PX; its
+  // 36 weights in registers, the input patch (PR rows x 34 columns x 4 channels) in LDS (float4 per
+  // pixel: one broadcast ds_read_b128 per pixel and tap), one coalesced 256-byte row of channels per
+  // pixel store
+  static_assert(PX == 32 || PX == 16, "conv_in: 32- or 16-pixel blocks");
+  constexpr int PR = PX == 32 ? 3 : 4, PP = PX / 4;
   __shared__ float ws[64][37];
-  __shared__ __attribute__((aligned(16))) float inl[3][34][4];
+  __shared__ __attribute__((aligned(16))) float inl[PR][34][4];
   __shared__ float2 red[4][2];
   const int tid = threadIdx.x, co = tid & 63, pg = tid >> 6;
   for (int i = tid; i < 64 * 36; i += 256) {
@@ -159,11 +164,11 @@ static __global__ __launch_bounds__(256) void conv_in_kernel(const ConvInParams 
     ws[o][k] = c < p.cin ? p.B[(size_t)o * p.kpad + tap * p.cin + c] : 0.f;
   }
   const int HW = p.H * p.W;
-  const int m0 = blockIdx.x * 32;
-  const int n = m0 / HW, r = m0 - n * HW, y = r / p.W, x0 = r - y * p.W;
+  const int m0 = blockIdx.x * PX;
+  const int n = m0 / HW, r = m0 - n * HW, y = r / p.W, x0 = PX == 32 ? r - y * p.W : 0;
   const int ns = p.n_mod ? n % p.n_mod : n;
-  for (int i = tid; i < 3 * 34 * 4; i += 256) {
-    const int c = i / 102, rem = i - c * 102, ry = rem / 34, cx = rem - ry * 34;
+  for (int i = tid; i < PR * 34 * 4; i += 256) {
+    const int c = i / (PR * 34), rem = i - c * (PR * 34), ry = rem / 34, cx = rem - ry * 34;
     const int iy = y + ry - 1, ix = x0 + cx - 1;
     const bool ok = iy >= 0 && iy < p.H && ix >= 0 && ix < p.W && c < p.creal;
     const float v = ok ? p.x[((size_t)ns * p.creal + c) * HW + (size_t)iy * p.W + ix] : 0.f;
@@ -176,12 +181,14 @@ static __global__ __launch_bounds__(256) void conv_in_kernel(const ConvInParams 
   float* o = p.out + (size_t)m0 * 64 + co;
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int px = 8 * pg + j;
+  for (int j = 0; j < PP; ++j) {
+    const int px = PP * pg + j;
+    // patch row / column of the pixel (PX = 16: the block's pixels continue on the next image row)
+    const int rr = PX == 32 ? 0 : (r - y * p.W + px) / p.W, cc = PX == 32 ? px : r - y * p.W + px - rr * p.W;
     float a = 0.f;
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {  // (tap, channel) order as the packed weights
-      const floatx4 v = *reinterpret_cast<const floatx4*>(&inl[tap / 3][px + tap % 3][0]);
+      const floatx4 v = *reinterpret_cast<const floatx4*>(&inl[rr + tap / 3][cc + tap % 3][0]);
 #pragma unroll
       for (int c = 0; c < 4; ++c) a = fmaf(w[tap * 4 + c], v[c], a);
     }
@@ -198,7 +205,7 @@ static __global__ __launch_bounds__(256) void conv_in_kernel(const ConvInParams 
   if ((tid & 31) == 0) red[pg][co >> 5] = make_float2(s1, s2);
   __syncthreads();
   if (tid < 2)
-    p.rowpart[((size_t)n * (HW / 32) + r / 32) * 2 + tid] =
+    p.rowpart[((size_t)n * (HW / PX) + r / PX) * 2 + tid] =
         make_float2((red[0][tid].x + red[1][tid].x) + (red[2][tid].x + red[3][tid].x),
                     (red[0][tid].y + red[1][tid].y) + (red[2][tid].y + red[3][tid].y));
 }

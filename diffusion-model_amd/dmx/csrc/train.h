@@ -215,8 +215,11 @@ static __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const GnBwdPar
 
 // Column sums: out[y][c] (+)= sum over rows [y rpb, min(R, (y + 1) rpb)) of in[r * stride + c];
 // grid (cdiv(C, 64), row blocks), 4 row groups x 64 columns per block, combined in a fixed order.
+// out_b != nullptr: columns >= cb go to out_b[c - cb] (two adjacent column ranges of one table, e.g. the
+// GroupNorm / LayerNorm gamma and beta gradients, summed by one launch)
 static __global__ __launch_bounds__(256) void colsum_kernel(const float* in, int R, int C, size_t stride, int rpb,
-                                                          float* out, int accumulate) {
+                                                          float* out, int accumulate, float* out_b = nullptr,
+                                                          int cb = 0) {
   __shared__ float red[4][64];
   const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
   const int r0 = blockIdx.y * rpb, r1 = min(R, r0 + rpb);
@@ -235,7 +238,7 @@ static __global__ __launch_bounds__(256) void colsum_kernel(const float* in, int
   __syncthreads();
   if (rg == 0 && c < C) {
     const float v = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
-    float* o = out + (size_t)blockIdx.y * C + c;
+    float* o = (out_b != nullptr && c >= cb) ? out_b + (c - cb) : out + (size_t)blockIdx.y * C + c;
     *o = accumulate ? *o + v : v;
   }
 }
@@ -798,45 +801,86 @@ __global__ __launch_bounds__(64 * KS) void attn_dkv_kernel(const float* qkv, con
 }
 
 // ---------------------------------------------------------------------------
-// Small dense layers (embedding MLPs, emb heads, GeomHead), R <= a few hundred rows:
+// Small dense layers (embedding MLPs, emb heads, GeomHead; R = the batch, a few hundred rows at most):
 //   forward y = x W^T + b over [R][K] -> [R][O]; backward dW = dY^T X, db = sum_r dY, dX = dY W.
-// One thread per output element, rows / inputs summed in order (deterministic).
+// All three are one strided small GEMM  C[i][j] = sum_l A(i, l) B(l, j),  A(i, l) = a[i sai + l sal],
+// B(l, j) = b[l sbl + j sbj]: 32 x 32 output tiles per 256-thread block (4 outputs per thread), the l
+// range in 32-deep chunks staged through LDS, split over grid.z where the output tiles alone leave the
+// chip empty (the emb heads' dX: 8 tiles, l = 1024 deep); each split writes its own partial slab and
+// small_gemm_finish_kernel adds the slabs in split order (+ bias, + accumulate).  Every output is a
+// fixed-order fp32 sum: deterministic.  (The previous one-thread-per-output kernels ran 32-block grids
+// with stride-K weight reads: 46 us per emb-head dX.)
 // ---------------------------------------------------------------------------
-static __global__ void dense_dw_kernel(const float* dy, int ldy, const float* x, int ldx, int R, int O, int K,
-                                       float* dw, float* db) {
-  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // grid covers O * K + O
-  if (i < (size_t)O * K) {
-    const int o = (int)(i / K), k = (int)(i % K);
-    float s = 0.f;
-    for (int r = 0; r < R; ++r) s += dy[(size_t)r * ldy + o] * x[(size_t)r * ldx + k];
-    dw[i] = s;
-  } else if (db != nullptr && i < (size_t)O * K + O) {
-    const int o = (int)(i - (size_t)O * K);
-    float s = 0.f;
-    for (int r = 0; r < R; ++r) s += dy[(size_t)r * ldy + o];
-    db[o] = s;
+struct SmallGemm {
+  const float* a;
+  const float* b;
+  long sai, sal, sbl, sbj;
+  int I, J, L, lsplit;  // lsplit: l per split (grid.z splits)
+  float* c;             // splits == 1: output [I][ldc] (+ bias, accumulate); else partial [z][I][J]
+  int ldc;
+  const float* bias;    // [J] or null
+  int accumulate;
+};
+static __global__ __launch_bounds__(256) void small_gemm_kernel(const SmallGemm g) {
+  __shared__ float As[32][33], Bs[32][33];  // [l][i], [l][j]
+  const int tid = threadIdx.x, tj = tid & 31, ti = tid >> 5;  // outputs (4 ti + q, tj)
+  const int i0 = blockIdx.y * 32, j0 = blockIdx.x * 32;
+  const int lb = blockIdx.z * g.lsplit, le = min(g.L, lb + g.lsplit);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int l0 = lb; l0 < le; l0 += 32) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + 256 * q;
+      // A tile: consecutive threads along whichever of i / l is contiguous in memory
+      const int ai = g.sai == 1 ? (e & 31) : (e >> 5), al = g.sai == 1 ? (e >> 5) : (e & 31);
+      const bool aok = i0 + ai < g.I && l0 + al < le;
+      As[al][ai] = aok ? g.a[(long)(i0 + ai) * g.sai + (long)(l0 + al) * g.sal] : 0.f;
+      const int bj = g.sbj == 1 ? (e & 31) : (e >> 5), bl = g.sbj == 1 ? (e >> 5) : (e & 31);
+      const bool bok = j0 + bj < g.J && l0 + bl < le;
+      Bs[bl][bj] = bok ? g.b[(long)(l0 + bl) * g.sbl + (long)(j0 + bj) * g.sbj] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int l = 0; l < 32; ++l) {
+      const float bv = Bs[l][tj];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[q] = fmaf(As[l][4 * ti + q], bv, acc[q]);
+    }
+    __syncthreads();
+  }
+  const int j = j0 + tj;
+  if (j >= g.J) return;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int i = i0 + 4 * ti + q;
+    if (i >= g.I) continue;
+    if (gridDim.z > 1) {
+      g.c[((size_t)blockIdx.z * g.I + i) * g.J + j] = acc[q];
+    } else {
+      float v = acc[q] + (g.bias != nullptr ? g.bias[j] : 0.f);
+      float* d = g.c + (size_t)i * g.ldc + j;
+      *d = g.accumulate ? *d + v : v;
+    }
   }
 }
-// dX[r][k] (+)= sum_o dY[r][o] W[o][k]  (W row-major [O][K])
-static __global__ void dense_dx_kernel(const float* dy, int ldy, const float* w, int R, int O, int K, float* dx, int ldx,
-                                       int accumulate) {
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < (size_t)R * K; i += (size_t)gridDim.x * 256) {
-    const int r = (int)(i / K), k = (int)(i % K);
-    float s = 0.f;
-    for (int o = 0; o < O; ++o) s += dy[(size_t)r * ldy + o] * w[(size_t)o * K + k];
-    float* d = dx + (size_t)r * ldx + k;
-    *d = accumulate ? *d + s : s;
+static __global__ void small_gemm_finish_kernel(const float* part, int splits, int I, int J, const float* bias,
+                                                float* c, int ldc, int accumulate) {
+  for (size_t e = (size_t)blockIdx.x * 256 + threadIdx.x; e < (size_t)I * J; e += (size_t)gridDim.x * 256) {
+    const int i = (int)(e / J), j = (int)(e % J);
+    float v = 0.f;
+    for (int z = 0; z < splits; ++z) v += part[(size_t)z * I * J + e];
+    v += bias != nullptr ? bias[j] : 0.f;
+    float* d = c + (size_t)i * ldc + j;
+    *d = accumulate ? *d + v : v;
   }
 }
-// y = x W^T + b (forward for the small layers of the training tape)
-static __global__ void dense_fwd_kernel(const float* x, int ldx, const float* w, const float* b, int R, int O, int K,
-                                        float* y, int ldy) {
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < (size_t)R * O; i += (size_t)gridDim.x * 256) {
-    const int r = (int)(i / O), o = (int)(i % O);
-    float s = b != nullptr ? b[o] : 0.f;
-    for (int k = 0; k < K; ++k) s += x[(size_t)r * ldx + k] * w[(size_t)o * K + k];
-    y[(size_t)r * ldy + o] = s;
-  }
+// db[o] = sum_r dY[r][o] (rows in order)
+static __global__ void dense_db_kernel(const float* dy, int ldy, int R, int O, float* db) {
+  const int o = blockIdx.x * 256 + threadIdx.x;
+  if (o >= O) return;
+  float s = 0.f;
+  for (int r = 0; r < R; ++r) s += dy[(size_t)r * ldy + o];
+  db[o] = s;
 }
 static __global__ void silu_fwd_kernel(const float* x, float* y, size_t n) {
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) y[i] = silu(x[i]);

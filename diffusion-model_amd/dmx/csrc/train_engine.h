@@ -198,11 +198,28 @@ static void ensure_train(dmx_model* m, hipStream_t st) {
 // ---------------------------------------------------------------------------
 // training forward
 // ---------------------------------------------------------------------------
+// C[I][J] (+)= A B (+ bias) through small_gemm_kernel (train.h), l split over grid.z until >= 256 blocks
+static void small_gemm(Run& R, SmallGemm g) {
+  const int tiles = cdiv(g.I, 32) * cdiv(g.J, 32);
+  int splits = std::max(1, std::min(cdiv(256, tiles), cdiv(g.L, 64)));
+  g.lsplit = cdiv(g.L, splits);
+  splits = cdiv(g.L, g.lsplit);
+  float* part = splits > 1 ? R.ws.get<float>((size_t)splits * g.I * g.J) : nullptr;
+  if (R.plan) return;
+  float* out = g.c;
+  if (splits > 1) g.c = part;
+  small_gemm_kernel<<<dim3(cdiv(g.J, 32), cdiv(g.I, 32), splits), 256, 0, R.st>>>(g);
+  HIPCHK(hipGetLastError());
+  if (splits > 1) {
+    small_gemm_finish_kernel<<<ew_blocks((size_t)g.I * g.J), 256, 0, R.st>>>(part, splits, g.I, g.J, g.bias, out, g.ldc,
+                                                                            g.accumulate);
+    HIPCHK(hipGetLastError());
+  }
+}
+// y[r][o] = b[o] + sum_k x[r][k] W[o][k]
 static void dense_fwd(Run& R, const float* x, int ldx, const float* w, const float* b, int rows, int O, int K, float* y,
                       int ldy) {
-  if (R.plan) return;
-  dense_fwd_kernel<<<ew_blocks((size_t)rows * O), 256, 0, R.st>>>(x, ldx, w, b, rows, O, K, y, ldy);
-  HIPCHK(hipGetLastError());
+  small_gemm(R, SmallGemm{x, w, ldx, 1, 1, K, rows, O, K, 0, y, ldy, b, 0});
 }
 
 static TRes train_res(Run& R, const ResW& w, const float* x, int N, int H, int W, bool residual, const float* emb,
@@ -421,17 +438,23 @@ static void train_fwd_body(Run& R, Tape& T, const TrainArgs& a) {
     T.hpre = R.ws.get<float>((size_t)N * m->cfg.ghid);
     T.hs = R.ws.get<float>((size_t)N * m->cfg.ghid);
   }
-  if (R.plan) return;
   R.layer = "train.heads";
-  out_head_kernel<<<dim3(cdiv(HW, 256), N), 256, 0, R.st>>>(T.feat, m->out_w, m->out_b, a.eps, m->in_ch, HW,
-                                                            m->range_flag);
-  HIPCHK(hipGetLastError());
-  if (geom) {
-    const int gh = m->cfg.ghid;
-    gap_fwd_kernel<<<N, 256, 0, R.st>>>(T.feat, HW, T.g);
-    dense_fwd(R, T.g, 64, srcp(m, "geom_head.mlp.0.weight"), srcp(m, "geom_head.mlp.0.bias"), N, gh, 64, T.hpre, gh);
-    silu_fwd_kernel<<<ew_blocks((size_t)N * gh), 256, 0, R.st>>>(T.hpre, T.hs, (size_t)N * gh);
+  if (!R.plan) {
+    out_head_kernel<<<dim3(cdiv(HW, 256), N), 256, 0, R.st>>>(T.feat, m->out_w, m->out_b, a.eps, m->in_ch, HW,
+                                                              m->range_flag);
     HIPCHK(hipGetLastError());
+  }
+  if (geom) {  // (dense_fwd runs in the plan pass too: its split partials are workspace allocations)
+    const int gh = m->cfg.ghid;
+    if (!R.plan) {
+      gap_fwd_kernel<<<N, 256, 0, R.st>>>(T.feat, HW, T.g);
+      HIPCHK(hipGetLastError());
+    }
+    dense_fwd(R, T.g, 64, srcp(m, "geom_head.mlp.0.weight"), srcp(m, "geom_head.mlp.0.bias"), N, gh, 64, T.hpre, gh);
+    if (!R.plan) {
+      silu_fwd_kernel<<<ew_blocks((size_t)N * gh), 256, 0, R.st>>>(T.hpre, T.hs, (size_t)N * gh);
+      HIPCHK(hipGetLastError());
+    }
     if (a.geom != nullptr)
       dense_fwd(R, T.hs, gh, srcp(m, "geom_head.mlp.2.weight"), srcp(m, "geom_head.mlp.2.bias"), N, m->cfg.gdim, gh,
                 a.geom, m->cfg.gdim);
@@ -452,6 +475,21 @@ static void colsum(Run& R, const float* in, int rows, int C, size_t stride, floa
   } else {
     colsum_kernel<<<dim3(cdiv(C, 64), nb), 256, 0, R.st>>>(in, rows, C, stride, rpb, part, 0);
     colsum_kernel<<<dim3(cdiv(C, 64), 1), 256, 0, R.st>>>(part, nb, C, C, nb, out, 0);
+  }
+  HIPCHK(hipGetLastError());
+}
+
+// outa[c] = sum of in[r][c], outb[c] = sum of in[r][C + c] (rows of 2C floats at `stride`): one launch
+// per level instead of two colsum calls
+static void colsum_pair(Run& R, const float* in, int rows, int C, size_t stride, float* outa, float* outb) {
+  const int rpb = 256, nb = cdiv(rows, rpb);
+  float* part = nb > 1 ? R.ws.get<float>((size_t)nb * 2 * C) : nullptr;
+  if (R.plan) return;
+  if (nb == 1) {
+    colsum_kernel<<<dim3(cdiv(2 * C, 64), 1), 256, 0, R.st>>>(in, rows, 2 * C, stride, rows, outa, 0, outb, C);
+  } else {
+    colsum_kernel<<<dim3(cdiv(2 * C, 64), nb), 256, 0, R.st>>>(in, rows, 2 * C, stride, rpb, part, 0);
+    colsum_kernel<<<dim3(cdiv(2 * C, 64), 1), 256, 0, R.st>>>(part, nb, 2 * C, 2 * C, nb, outa, 0, outb, C);
   }
   HIPCHK(hipGetLastError());
 }
@@ -513,8 +551,7 @@ static void gn_bwd(Run& R, const float* r, const float2* rp, int nseg, int rrows
   float* bch = R.ws.get<float>((size_t)N * chunks * 3 * C);
   if (!R.plan) gn_bwd_launch(R, r, rp, nseg, rrows, g, b, res, act, dout, N, C, HW, dr, dres, dres_mode, sums, chpart,
                              demb, demb_stride, demb_off, ppb, bsum, bch);
-  colsum(R, chpart, N, C, 2 * (size_t)C, ggamma);
-  colsum(R, chpart + C, N, C, 2 * (size_t)C, gbeta);
+  colsum_pair(R, chpart, N, C, 2 * (size_t)C, ggamma, gbeta);
 }
 
 static void gn_bwd_launch(Run& R, const float* r, const float2* rp, int nseg, int rrows, const Vec& g, const Vec& b,
@@ -573,8 +610,7 @@ static void ln_bwd(Run& R, const float* x, const Vec& w, const float* dy, float*
     R.end();
     HIPCHK(hipGetLastError());
   }
-  colsum(R, part, blocks, C, 2 * (size_t)C, gw);
-  colsum(R, part + C, blocks, C, 2 * (size_t)C, gb);
+  colsum_pair(R, part, blocks, C, 2 * (size_t)C, gw, gb);
 }
 
 static void attn_core_bwd(Run& R, const float* qkv, const float* o, const float* dout, float* dqkv, int N, int L,
@@ -664,17 +700,18 @@ static void zero_grad(Run& R, const GradMap& G, dmx_model* m, const std::string&
     }
 }
 
+// dW[o][k] = sum_r dY[r][o] x[r][k], db[o] = sum_r dY[r][o]
 static void dense_dw(Run& R, const float* dy, int ldy, const float* x, int ldx, int rows, int O, int K, float* dw,
                      float* db) {
-  if (R.plan) return;
-  dense_dw_kernel<<<cdiv(O * K + O, 256), 256, 0, R.st>>>(dy, ldy, x, ldx, rows, O, K, dw, db);
+  small_gemm(R, SmallGemm{dy, x, 1, ldy, ldx, 1, O, K, rows, 0, dw, K, nullptr, 0});
+  if (R.plan || db == nullptr) return;
+  dense_db_kernel<<<cdiv(O, 256), 256, 0, R.st>>>(dy, ldy, rows, O, db);
   HIPCHK(hipGetLastError());
 }
+// dX[r][k] (+)= sum_o dY[r][o] W[o][k]
 static void dense_dx(Run& R, const float* dy, int ldy, const float* w, int rows, int O, int K, float* dx, int ldx,
                      bool accumulate) {
-  if (R.plan) return;
-  dense_dx_kernel<<<ew_blocks((size_t)rows * K), 256, 0, R.st>>>(dy, ldy, w, rows, O, K, dx, ldx, accumulate ? 1 : 0);
-  HIPCHK(hipGetLastError());
+  small_gemm(R, SmallGemm{dy, w, ldy, 1, K, 1, rows, K, O, 0, dx, ldx, nullptr, accumulate ? 1 : 0});
 }
 
 static void train_bwd_body(Run& R, Tape& T, const GradMap& G, const float* d_eps, const float* d_geom) {
