@@ -64,6 +64,9 @@ namespace dmx {
 #ifndef DMX_WSHFL
 #define DMX_WSHFL 0
 #endif
+#ifndef DMX_WHSW  // (A/B build) bank-conflict-free pixel order of the halo stores
+#define DMX_WHSW 1
+#endif
 #ifndef DMX_WEPP
 #define DMX_WEPP 34
 #endif
@@ -219,10 +222,29 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   for (int k = 0; k < NPI; ++k) {
     const int e = tid + 512 * k;
     const int h = e >> 2, q = e & 3;
+    // halo row (all stacked samples) and column of pixel slot h.  The 8-lane groups of ds_write_b128
+    // (two pixels each) must cover 32 distinct banks: the two pixels' 16-float pieces must sit 16 mod
+    // 32 floats apart.  W = 32 (4 RP = 0 mod 32): columns c and c + 8 of one row (10 pixel-pitches
+    // of 20 floats apart: 16 mod 32); W = 16 / 8 (8 RP = 16 mod 32): one column in rows 2t, 2t + 1.
+    // Plain row-major slots put parity-plane neighbours on the same banks (2-way conflicts on every
+    // halo store).
+    int hrow, hcol;
+    if constexpr (!DMX_WHSW || RING0) {
+      hrow = h / HC;
+      hcol = h - hrow * HC;
+    } else if constexpr (W == 32) {
+      const int pr = (h >> 1) % 17, m = h & 1;  // 17 pixel pairs per 34-column row
+      hrow = (h >> 1) / 17;
+      hcol = pr < 8 ? pr + 8 * m : pr < 16 ? 8 + pr + 8 * m : 32 + m;
+    } else {
+      const int t = (h >> 1) / HC;  // HR is even: row pairs
+      hcol = (h >> 1) - t * HC;
+      hrow = 2 * t + (h & 1);
+    }
     // stacked sample, halo row inside it, halo column (RING0: interior pixel h of the block's samples)
-    const int sh = RING0 ? h >> 4 : (h / HC) / PS;
-    const int ry = RING0 ? ((h >> 2) & 3) + 1 : h / HC - sh * PS;
-    const int hx = RING0 ? (h & 3) + 1 : h - (h / HC) * HC;
+    const int sh = RING0 ? h >> 4 : hrow / PS;
+    const int ry = RING0 ? ((h >> 2) & 3) + 1 : hrow - sh * PS;
+    const int hx = RING0 ? (h & 3) + 1 : hcol;
     const int y = y0 + ry - 1, x = hx - 1;
     const bool ok = e < NPC && ry < HRS && y >= 0 && y < p.H && x >= 0 && x < WA && nsmp + sh < nsamp;
     hoff[k] = ok ? ((((nsmp + sh) * p.H + y) * WA + x) * C + q * 4) : -1;
@@ -293,7 +315,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
     for (int k = 0; k < NPI; ++k) {
       floatx4 v = ha[k];
       if constexpr (GNA && !(DMX_WDIAG & 4)) {  // GroupNorm (+ residual) + GELU of the raw source; zero padding stays zero
-        const float2 gst = gst_s[SPB == 1 ? 0 : min(((tid + 512 * k) >> 2) / HC / PS, SPB - 1)];
+        const float2 gst = gst_s[SPB == 1 ? 0 : min(hls[k] / SQ, SPB - 1)];  // (the piece's stacked sample)
         v = gn_apply4v(v, gst, ggam, gbet, GNA == 1 ? 1 : 0);
         if constexpr (GNA == 2) {
 #pragma unroll
