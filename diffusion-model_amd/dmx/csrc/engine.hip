@@ -1604,16 +1604,21 @@ static bool tok_frag_enabled() {
   }();
   return v;
 }
-// DMX_TOK_WIDE (same-box A/B): 1 the C = 256 QKV runs tok_ln_qkv_w_kernel (8-wave blocks, 384 columns,
-// one round of blocks); 0 (default) the 4-wave 64-column tok_ln_qkv_kernel — the wide kernel measured
-// -0.2 % per CFG step (3 / 3 same-box rounds): fewer LayerNorm recomputes and blocks do not pay for
-// its one block per CU.
-static bool tok_qkv_wide() {
-  static const bool v = [] {
+// DMX_TOK_WIDE (same-box A/B): whether the C = 256 QKV runs tok_ln_qkv_w_kernel (8-wave blocks, 384
+// columns, the LayerNorm of a token tile twice instead of twelve times) instead of the 4-wave 64-column
+// tok_ln_qkv_kernel.  0 = never, 1 = always (-0.2 % per CFG step, 3 / 3 same-box rounds), 2 (default) =
+// where its grid (two column halves per 64-token tile) still fills the chip: sa2 (8192 tokens: 35 vs
+// 41 us eager), not sa3 (2048 tokens: 32 vs 14 us).
+static int tok_qkv_wide_mode() {
+  static const int v = [] {
     const char* e = std::getenv("DMX_TOK_WIDE");
-    return e != nullptr && std::atoi(e) != 0;
+    return e == nullptr ? 2 : std::atoi(e);
   }();
   return v;
+}
+static bool tok_qkv_wide(int M) {
+  const int m = tok_qkv_wide_mode();
+  return m == 1 || (m == 2 && cdiv(M, 64) * 2 >= 256);
 }
 static TokW tokw(const ConvW& c) {
   return TokW{c.Bh, c.Bl, c.bias, c.inv_scale, c.kpad, tok_frag_enabled() ? c.Fh : nullptr,
@@ -1647,7 +1652,7 @@ static float* attn_block_fused(Run& R, const AttnW& a, const float* x, int N, in
                   std::to_string(x1) + ">",
               2.0 * M * C * 3.0 * C, 16.0 * (double)M * C);
       launch_tok_qkv_lds(C, tpb, x1, tp, gl, R.st);
-    } else if (tok_qkv_wide()) {
+    } else if (tok_qkv_wide(M)) {
       // C = 256: 8-wave blocks of 64 tokens x 384 columns (one round of blocks, LayerNorm twice per tile)
       const dim3 grid(cdiv(M, 64), 2);
       R.begin("tok_ln_qkv_w_kernel<" + cs + ", 384, 8, 4, " + std::to_string(x1) + ">", 2.0 * M * C * 3.0 * C,
