@@ -84,13 +84,14 @@ def test_unet_forward_vs_oracle_no_cond(model, cuda, unet_sd):
     assert rel(eps, e2) < TOL and rel(geom, g2) < TOL
 
 
-@pytest.mark.parametrize("hw", [32, 28])
+@pytest.mark.parametrize("hw", [32, 28, 20])
 def test_unet_forward_bench_batch_vs_oracle(model, cuda, unet_sd, prec, hw):
     """One forward of 128 samples (the CFG batch of B=64): the batch at which the 16x16 / 32x32 convs
     take their large-grid kernels — in x3 mode the Winograd F(2x2, 3x3) convs (igemm_wino.h) — checked
     on eps itself (a CFG step's latent hides eps errors behind its (1-a)/sqrt(1-ab) factor).  28x28:
     the 28 / 14 / 7 / 3 maps in the Winograd geometries of 32 / 16 / 8 / 4 (zero-padded rows and
-    columns, partial GroupNorm rows) and the Up path's pad."""
+    columns, partial GroupNorm rows) and the Up path's pad; 20x20: 20 / 10 / 5 / 2 maps (a 2 x 2 map in
+    the 4-wide geometry, 5 x 5 in the 8-wide one, 3 bands of which the last holds 4 rows)."""
     g = torch.Generator().manual_seed(128 + hw)
     N = 128
     x = torch.randn((N, 4, hw, hw), generator=g)
