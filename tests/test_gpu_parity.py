@@ -429,18 +429,18 @@ def test_uncond_sample_latent_T100_golden(golden, cuda):
     assert rel(z, g["latent"]) < 1e-4
 
 
-@pytest.mark.parametrize("B", [4, 64])
-def test_graph_loop_equals_eager_and_is_deterministic(model, cuda, B):
+@pytest.mark.parametrize("B,hw", [(4, 32), (64, 32), (64, 28)])
+def test_graph_loop_equals_eager_and_is_deterministic(model, cuda, B, hw):
     """Device-noise mode: hipGraph replay == eager launches, bit for bit, and reruns are identical
     (19 steps: two launches of the 8-step graph and three of the one-step graph).  B = 64 is the
     benchmark's timed region (bench.py: the 8-step graph at B = 64 — Winograd convs, Philox noise,
-    cond-MLP rows computed once per graph)."""
+    cond-MLP rows computed once per graph); (64, 28): bench.py's latent28 leg."""
     from dmx import engine  # noqa: F401
     import diff
     d = diff.Diffuser(1000, device=cuda)
     nm = model.native()
     g = torch.Generator().manual_seed(2)
-    x0 = torch.randn((B, 4, 32, 32), generator=g).to(cuda)
+    x0 = torch.randn((B, 4, hw, hw), generator=g).to(cuda)
     y = torch.tensor([1 + i % 3 for i in range(B)], device=cuda)
     vals = torch.rand((B, 12), generator=g).to(cuda)
     mask = (torch.rand((B, 12), generator=g) > 0.3).float().to(cuda) if B > 4 else torch.ones((B, 12), device=cuda)
