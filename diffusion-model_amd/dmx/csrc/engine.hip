@@ -709,12 +709,21 @@ struct Prof {
 // recorded; at the end of the step the sums are compared with the previous step's and the first
 // layer after which they differ is printed (a race localiser: identical inputs must give identical
 // sums).
+// Diagnostic builds only (-DDMX_DIAG=1, e.g. `build.py --out libdiag.so -- -DDMX_DIAG=1`): product
+// builds take no such switch.
+#ifndef DMX_DIAG
+#define DMX_DIAG 0
+#endif
 static bool cksum_enabled() {
+#if DMX_DIAG
   static const bool v = [] {
     const char* e = std::getenv("DMX_CKSUM");
     return e != nullptr && std::atoi(e) != 0;
   }();
   return v;
+#else
+  return false;
+#endif
 }
 static __global__ void cksum_kernel(const unsigned* p, size_t n, unsigned long long* slot) {
   unsigned long long s = 0;
@@ -786,49 +795,28 @@ static bool split_a_enabled() { return true; }
 
 // Max-pool / up-concat sources also written as f16 planes for the next conv1 (split GEMM A;
 // measured +0.2 %, same-box A/B) — they stay fp32 too, as the residual of that ResBlock.
-// DMX_CAT_PLANES (same-box A/B): 1 planes for every pooled / up-concat source; 0 none; 2 (default)
-// none where conv1 runs a halo conv, which splits an fp32 source while staging — the source is
-// written once (fp32, also the block's residual) instead of twice: prep_kernel<3> at 32 x 32
-// 41.5 -> 32.9 us, the convs unchanged, +1.3 % per CFG step over 1 (same-box A/B).
-static int cat_planes_mode() {
-  static const int v = [] {
-    const char* e = std::getenv("DMX_CAT_PLANES");
-    return e == nullptr ? 2 : std::atoi(e);
-  }();
-  return v;
-}
-static bool cat_planes_enabled() { return cat_planes_mode() != 0; }
+// Planes are skipped where conv1 runs a halo / Winograd conv, which splits an fp32 source while
+// staging — the source is written once (fp32, also the block's residual) instead of twice:
+// prep_kernel<3> at 32 x 32 41.5 -> 32.9 us, the convs unchanged, +1.3 % per CFG step over planes
+// for every source (same-box A/B, round 3; the switch was removed in round 6).
+static bool cat_planes_enabled() { return true; }
 
 // The 512-thread ping-pong kernel for the large f16-plane convs (measured +1.3 % over the
 // two-block kernel, same-box A/B).
 static bool pp_enabled() { return true; }
 
-// The halo-staged 3x3 conv (igemm_halo.h) for the large 16x16 / 32x32 convs.  DMX_HALO (same-box
-// A/B): 4 (default) B staged in LDS per step, 16-wave blocks (4 x 4 waves of 64 x 32 at BN = 128,
-// 8 x 2 of 32 x 32 at BN = 64) — +2.1 % per CFG step over 2; 2: the same with 8-wave blocks
-// (4 x 2 waves) — +2.4 … +2.7 % over the ping-pong / register-staged kernels it replaced; 5: BN =
-// 128 as 8 x 2 waves of 32 x 64 (between 2 and 4); 1: B read straight into registers (fragment-
-// ordered planes, one barrier per chunk) — at parity with the old kernels; 0: off.
-static int halo_mode() {
-  static const int v = [] {
-    const char* e = std::getenv("DMX_HALO");
-    return e == nullptr ? 4 : std::atoi(e);
-  }();
-  return v;
-}
-static bool halo_enabled() { return halo_mode() != 0; }
-// Grids with fewer blocks than this split K (DMX_SPLIT_BELOW, same-box A/B).  256 (one block per CU):
-// since the low-resolution convs moved to the halo kernels (own split rule), this only decides the
-// 16 x 16 convs of the CFG-shared down1 stage (256 blocks): unsplit, their GroupNorm runs as
-// norm_kernel over many blocks instead of reduce_norm_kernel's one block per sample (+0.25 % per CFG
-// step over 512, 3/3 same-box rounds).
-static int split_below() {
-  static const int v = [] {
-    const char* e = std::getenv("DMX_SPLIT_BELOW");
-    return e == nullptr ? 256 : std::atoi(e);
-  }();
-  return v;
-}
+// The halo-staged 3x3 conv (igemm_halo.h) for the large 16x16 / 32x32 convs (the small-batch class;
+// batches of >= 64 samples run Winograd): B staged in LDS per step, 16-wave blocks (4 x 4 waves of
+// 64 x 32 at BN = 128, 8 x 2 of 32 x 32 at BN = 64) — +2.1 % per CFG step over 8-wave blocks, which
+// were +2.4 … +2.7 % over the ping-pong / register-staged kernels it replaced (round 3 A/Bs; the
+// losing layouts were removed in round 6).
+constexpr int HALO_MODE = 4;
+static bool halo_enabled() { return true; }
+// Grids with fewer blocks than this split K: 256 (one block per CU).  Since the low-resolution convs
+// moved to the halo kernels (own split rule), this only decides the implicit GEMMs of small
+// batches; unsplit 256-block grids run their GroupNorm as norm_kernel over many blocks instead of
+// reduce_norm_kernel's one block per sample (+0.25 % per CFG step over 512, 3/3 same-box rounds).
+static int split_below() { return 256; }
 // reduce_norm_kernel runs with at least two float4 per thread (KV >= 2; the 4x4 C = 256 ResBlocks,
 // 1024 float4 per sample, leave the second one idle).  The one-float4 instance (KV = 1) gave
 // run-to-run different outputs while a second process shared the GPU (tools/conc_step.sh +
@@ -838,21 +826,11 @@ static int split_below() {
 // scalar loads of data, the producer covers every slab element — DMX_POISON), so the instance is not
 // compiled at all: no knob can select it.
 constexpr int RN_MIN_KV = 2;
-// DMX_RN_FUSE (race bisection): 0 = split-K slabs reduced by splitk_reduce_kernel + norm_kernel
-static bool rn_fuse_enabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("DMX_RN_FUSE");
-    return e == nullptr || std::atoi(e) != 0;
-  }();
-  return v;
-}
-static bool gn_fuse_enabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("DMX_GN_FUSE");
-    return e == nullptr || std::atoi(e) != 0;
-  }();
-  return v;
-}
+// Split-K slabs of a ResBlock conv go straight into reduce_norm_kernel (slab sum + GroupNorm in one
+// launch), and the mid-ResBlock GroupNorm + GELU is folded into conv2's staging where that pays
+// (DMX_RN_FUSE / DMX_GN_FUSE A/B and bisection switches until round 5: always on since).
+static bool rn_fuse_enabled() { return true; }
+static bool gn_fuse_enabled() { return true; }
 
 // Implicit GEMM: conv3x3 (taps 9), ConvT phases (taps 4, phases 4), conv4x4-s2 (taps 16),
 // linear (taps 1).  Sources are plain NHWC (or the NCHW network input); grids too small to
@@ -920,13 +898,7 @@ struct GnLoad {
 // of splits * M * Cout floats (workspace linear in the batch, test_large_batch_class_is_shard_exact
 // bounds it) instead of whole-K tiles.  A coarser class above 128 would put a 64-per-rank shard and its
 // parent batch in different classes and lose config 3's bit-identical shards.
-static int dec_n(const Run& R, int N) {
-  static const bool per_batch = [] {  // DMX_DEC_N=0 (A/B): decisions from the batch itself
-    const char* e = std::getenv("DMX_DEC_N");
-    return e != nullptr && std::atoi(e) == 0;
-  }();
-  return R.tile_n > 0 ? R.tile_n : (N >= 64 && !per_batch) ? 128 : N;
-}
+static int dec_n(const Run& R, int N) { return R.tile_n > 0 ? R.tile_n : N >= 64 ? 128 : N; }
 
 // Output-channel tile of the halo-staged 3x3 conv for this GEMM, or 0 when it does not apply
 // (igemm_halo.h: 256-pixel tiles of whole rows of one sample, W = 16 / 32, 32-channel chunks,
@@ -942,69 +914,19 @@ static int halo_bn(const Run& R, int src_C, int N, int H, int W, const ConvW& cw
   return 0;
 }
 
-// DMX_HALO_MS (same-box A/B): 0 low-resolution halo conv off (implicit GEMM + split-K); 1 per-tap
-// pipeline only (igemm_halo_kernel MS); 2 chunk-staged BN = 64 kernel (igemm_halo_cs_kernel), the
-// per-tap BN = 128 kernel where that fills 256 blocks (8 x 8, Cout >= 512); 3 (default) chunk-staged
-// everywhere (measured +1.5 % per CFG step over 0, same-box A/B; 1 and 2 in between).
-static int halo_ms_mode() {
-  static const int v = [] {
-    const char* e = std::getenv("DMX_HALO_MS");
-    return e == nullptr ? 3 : std::atoi(e);
-  }();
-  return v;
-}
-static bool halo_ms_enabled() { return halo_ms_mode() != 0; }
+// Low-resolution halo conv (8 x 8 / 4 x 4, the small-batch class): the chunk-staged kernel
+// (igemm_halo_cs_kernel) everywhere — +1.5 % per CFG step over implicit GEMM + split-K; the per-tap
+// pipeline and mixed layouts measured in between (round 3 A/Bs; removed in round 6).
+static bool halo_ms_enabled() { return true; }
 
 // GELU form of the exact-fp32 mode (training forward, fp32 reference mode): the erf form, as the
-// reference.  DMX_EXACT_GELU=fit (VERDICT r3 item 7 study, tools/gelu_train_study.py) runs the
-// inference fit there too.
-static int gelu_exact_flag(const Run& R) {
-  static const bool fit = [] {
-    const char* e = std::getenv("DMX_EXACT_GELU");
-    return e != nullptr && std::string(e) == "fit";
-  }();
-  return R.m->prec == 0 && !fit ? 1 : 0;
-}
+// reference (the fit's own effect on the training gradients was measured at <= 7.8e-8).
+static int gelu_exact_flag(const Run& R) { return R.m->prec == 0 ? 1 : 0; }
 
-// DMX_WINO (same-box A/B): 1 (default) the halo convs at 16x16 / 32x32 run as Winograd F(2x2, 3x3)
-// (igemm_wino.h) in the x3 mode; 0 keeps the direct halo kernels.
-static bool wino_enabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("DMX_WINO");
-    return e == nullptr || std::atoi(e) != 0;
-  }();
-  return v;
-}
-// The Winograd conv (x3 fp32-semantics mode, fp32 source, 64-tile x 64-channel blocks, 16-channel
-// chunks) replaces a halo conv (hbn > 0: 16 x 16 / 32 x 32) or, on 8 x 8 maps, the low-resolution
-// halo conv where 4-sample blocks fill >= 256 blocks without split-K (up1.0: 512 -> 512).
-// DMX_WINO_SPLIT (same-box A/B): 1 (default) Winograd also for the convs whose 64 x 64 blocks do
-// not fill 256 CUs, with K split over 16-channel chunks (slabs reduced like the other split convs).
-static bool wino_split_enabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("DMX_WINO_SPLIT");
-    return e == nullptr || std::atoi(e) != 0;
-  }();
-  return v;
-}
-// DMX_WINO_F16 (A/B): 1 (default) the fp16 mode (config 4, precision 2) runs the Winograd convs too
-// (X1 instances: U hi and V rounded to f16, one MFMA per product); 0 keeps its direct kernels.
-static bool wino_f16_enabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("DMX_WINO_F16");
-    return e == nullptr || std::atoi(e) != 0;
-  }();
-  return v;
-}
-// DMX_WINO_MASK (bisection aid / A/B): bit 0 / 1 / 2 / 3 allow the Winograd conv at W = 8 / 16 / 32 / 4
-// (default 15)
-static int wino_mask() {
-  static const int v = [] {
-    const char* e = std::getenv("DMX_WINO_MASK");
-    return e == nullptr ? 15 : std::atoi(e);
-  }();
-  return v;
-}
+// The Winograd conv (x3 fp32-semantics and fp16 modes, fp32 source, 64-tile x 64-channel blocks,
+// 16-channel chunks) replaces the halo convs for batches of >= 64 samples, with K split over 16-channel
+// chunks where the 64 x 64 blocks do not fill 256 CUs (slabs reduced like the other split convs).
+// (DMX_WINO / DMX_WINO_SPLIT / DMX_WINO_F16 / DMX_WINO_MASK A/B switches until round 5.)
 // Winograd plan of a 3x3 conv given an fp32 source: 0 = not applicable, else the K split count
 // (1 = whole K) and *cps = 16-channel chunks per split.  Blocks: 64 tiles (8 rows of a 32-wide map,
 // one 16 x 16 sample, four 8 x 8 samples or sixteen 4 x 4 samples — the last block of a batch that
@@ -1026,13 +948,12 @@ static int wino_blocks(int G, int N, int H) {  // blocks along the pixel axis
 }
 static int wino_plan(const Run& R, int src_C, int N, int H, int W, const ConvW& cw, int* cps) {
   // (U-Net only: the VAE decoder keeps its per-sample-tiled direct convs, Run::tile_n)
-  if (!wino_enabled() || R.m->prec < 1 || (R.m->prec == 2 && !wino_f16_enabled()) || R.m->kind == DMX_VAE ||
+  if (R.m->prec < 1 || R.m->kind == DMX_VAE ||
       R.tile_n > 0 || cw.Uh == nullptr ||
       cw.phases != 1 || cw.taps != 9)
     return 0;
   const int G = wino_geom(H, W);
   if (G == 0) return 0;
-  if (!((wino_mask() >> (G == 8 ? 0 : G == 16 ? 1 : G == 32 ? 2 : 3)) & 1)) return 0;
   if (src_C % 16 != 0 || cw.cout % 64 != 0 || (size_t)16 * cw.cout * src_C * 2 >= ((size_t)1 << 31)) return 0;
   const int nref = dec_n(R, N) >= 64 ? 128 : 2;
   const int blocks = wino_blocks(G, nref, H) * (cw.cout / 64), nch = src_C / 16;
@@ -1040,7 +961,7 @@ static int wino_plan(const Run& R, int src_C, int N, int H, int W, const ConvW& 
   if (blocks < 256) {
     // (small-batch class: the split Winograd conv lost to the direct kernels — config 5, B = 1 CFG:
     // 1.44 vs 1.31 ms per step, same box)
-    if (!wino_split_enabled() || nref < 128) return 0;
+    if (nref < 128) return 0;
     sp = std::max(1, std::min(nch, cdiv(256, blocks)));
     cp = cdiv(nch, sp);
     sp = cdiv(nch, cp);
@@ -1057,7 +978,9 @@ static bool wino_any(const Run& R, int src_C, int N, int H, int W, const ConvW& 
 // build without it: -11 % per step).  Same-box per-conv A/B against a norm_kernel pass + plain
 // staging: Cout = 64 GN + GELU fused wins (-8 us at 32x32, -6 us at 16x16 split), Cout = 128 even,
 // Cout >= 256 and every GroupNorm-residual-GELU (which also reads the residual) lose 10-42 us.
-static bool wino_gna_pays(const ConvW& cw, int gna) { return gna == 1 && cw.cout <= 64; }
+// The 4-wide geometry has no GroupNorm-on-load instances (split-K only), so a conv on a map of width
+// <= 4 never takes it (the launcher would throw mid-forward otherwise).
+static bool wino_gna_pays(const ConvW& cw, int gna, int W) { return gna == 1 && cw.cout <= 64 && wino_geom(1, W) != 4; }
 
 // Low-resolution halo conv (igemm_halo.h, W = 8 / 4 square maps): 256-pixel tiles of whole samples,
 // K split over 32-channel chunks until the grid has >= 256 blocks.  Returns the output-channel tile
@@ -1081,8 +1004,7 @@ static int halo_ms_bn(const Run& R, int src_C, int N, int H, int W, const ConvW&
     return tiles * sp;
   };
   int sp = 1, cp = nch, bn = 0;
-  if (halo_ms_mode() != 3 && W == 8 && cw.cout % 128 == 0 && plan(128, sp, cp) >= 256) bn = 128;
-  else if (cw.cout % 64 == 0) {
+  if (cw.cout % 64 == 0) {
     plan(64, sp, cp);
     bn = 64;
   }
@@ -1268,7 +1190,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   if (msbn) {  // low-resolution halo conv: 256-pixel tiles of whole samples (igemm_halo.h MS)
     const int e = splits > 1 ? (int)EPI_PARTIAL : (int)EPI_STATS;
     dim3 gm(cdiv(M, 256), cw.cout / msbn, splits);
-    const bool cs = msbn == 64 && halo_ms_mode() >= 2;
+    const bool cs = msbn == 64;
     if (cs) std::snprintf(nm, sizeof nm, "igemm_halo_cs_kernel<%d, %d, %d, %d>", e, sa, x1 ? 1 : 0, W);
     else std::snprintf(nm, sizeof nm, "igemm_halo_kernel<%d, %d, %d, %d, %d, 0>", msbn, e, sa, x1 ? 1 : 0, W);
     R.begin(nm, flops, bytes + (splits > 1 ? 4.0 * splits * M * cw.cout : 0.0));
@@ -1337,7 +1259,7 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
     std::snprintf(nm, sizeof nm, "igemm_halo_kernel<%d, %d, %d, %d, %d, %d>", hbn, (int)EPI_STATS, sa, x1 ? 1 : 0, W,
                   gna);
     R.begin(nm, flops, bytes);
-    launch_halo(halo_mode(), hbn, W, sa, x1 ? 1 : 0, gna, xp, gh, R.st);
+    launch_halo(HALO_MODE, hbn, W, sa, x1 ? 1 : 0, gna, xp, gh, R.st);
     R.end();
     HIPCHK(hipGetLastError());
     return rrows;
@@ -1497,7 +1419,7 @@ static float* resblock(Run& R, const ResW& w, const SrcDesc& in, int mode, int N
   // no hi / lo planes.  DMX_GN_FUSE=0 turns it off (the staged operand is the same either way).
   const bool fuse1 = gn_fuse_enabled() && !d1.fused && !R.m->debug &&
                      ((planes && halo_bn(R, w.mid, N, H, W, w.c2, EPI_STATS, true) > 0) ||
-                      (c2_wino && wino_gna_pays(w.c2, 1)));
+                      (c2_wino && wino_gna_pays(w.c2, 1, W)));
   int rr2;
   if (fuse1) {
     GnLoad g;
@@ -1595,35 +1517,15 @@ static void attention_core(Run& R, const float* qkv, float* out, int N, int L, i
   HIPCHK(hipGetLastError());
 }
 
-// DMX_TOK_FRAG=0: token kernels read B fragments from the [Npad][Kpad] planes (32 rows per load)
-// instead of the fragment-ordered copies (same-box A/B).
-static bool tok_frag_enabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("DMX_TOK_FRAG");
-    return e == nullptr || std::atoi(e) != 0;
-  }();
-  return v;
-}
-// DMX_TOK_WIDE (same-box A/B): whether the C = 256 QKV runs tok_ln_qkv_w_kernel (8-wave blocks, 384
-// columns, the LayerNorm of a token tile twice instead of twelve times) instead of the 4-wave 64-column
-// tok_ln_qkv_kernel.  0 = never, 1 = always (-0.2 % per CFG step, 3 / 3 same-box rounds), 2 (default) =
-// where its grid (two column halves per 64-token tile) still fills the chip: sa2 (8192 tokens: 35 vs
-// 41 us eager), not sa3 (2048 tokens: 32 vs 14 us).
-static int tok_qkv_wide_mode() {
-  static const int v = [] {
-    const char* e = std::getenv("DMX_TOK_WIDE");
-    return e == nullptr ? 2 : std::atoi(e);
-  }();
-  return v;
-}
-static bool tok_qkv_wide(int M) {
-  const int m = tok_qkv_wide_mode();
-  return m == 1 || (m == 2 && cdiv(M, 64) * 2 >= 256);
-}
-static TokW tokw(const ConvW& c) {
-  return TokW{c.Bh, c.Bl, c.bias, c.inv_scale, c.kpad, tok_frag_enabled() ? c.Fh : nullptr,
-              tok_frag_enabled() ? c.Fl : nullptr};
-}
+// Whether the C = 256 QKV runs tok_ln_qkv_w_kernel (8-wave blocks, 384 columns, the LayerNorm of a
+// token tile twice instead of twelve times) instead of the 4-wave 64-column tok_ln_qkv_kernel: where
+// its grid (two column halves per 64-token tile) still fills the chip — sa2 (8192 tokens: 35 vs 41 us
+// eager), not sa3 (2048 tokens: 32 vs 14 us); everywhere was -0.2 % per CFG step (round 5 A/B).
+// The choice follows the batch class (dec_n), not the raw token count, so a batch and its shards take
+// the same kernel.  The two kernels also compute every output identically (the same
+// tok_rows LayerNorm, the same k-step order), which test_large_batch_class_is_shard_exact guards.
+static bool tok_qkv_wide(const Run& R, int N, int L) { return cdiv(dec_n(R, N) * L, 64) * 2 >= 256; }
+static TokW tokw(const ConvW& c) { return TokW{c.Bh, c.Bl, c.bias, c.inv_scale, c.kpad, c.Fh, c.Fl}; }
 
 // Fused token kernels (tokmlp.h) for the split-precision modes: TA -> attention core -> TB.
 static float* attn_block_fused(Run& R, const AttnW& a, const float* x, int N, int H, int W) {
@@ -1652,7 +1554,7 @@ static float* attn_block_fused(Run& R, const AttnW& a, const float* x, int N, in
                   std::to_string(x1) + ">",
               2.0 * M * C * 3.0 * C, 16.0 * (double)M * C);
       launch_tok_qkv_lds(C, tpb, x1, tp, gl, R.st);
-    } else if (tok_qkv_wide(M)) {
+    } else if (tok_qkv_wide(R, N, L)) {
       // C = 256: 8-wave blocks of 64 tokens x 384 columns (one round of blocks, LayerNorm twice per tile)
       const dim3 grid(cdiv(M, 64), 2);
       R.begin("tok_ln_qkv_w_kernel<" + cs + ", 384, 8, 4, " + std::to_string(x1) + ">", 2.0 * M * C * 3.0 * C,
@@ -1820,7 +1722,7 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
     const size_t pool_el = (size_t)nb * nh * nw * cc;
     float* pooled = R.ws.get<float>(pool_el);
     const bool pool_planes = R.m->prec >= 1 && m->down[i].r0.c1.Bh != nullptr && !R.m->debug && cat_planes_enabled() &&
-                             !(cat_planes_mode() == 2 && (halo_bn(R, cc, nb, nh, nw, m->down[i].r0.c1, EPI_STATS, true) > 0 ||
+                             !((halo_bn(R, cc, nb, nh, nw, m->down[i].r0.c1, EPI_STATS, true) > 0 ||
                                                           halo_ms_bn_any(R, cc, nb, nh, nw, m->down[i].r0.c1))) &&
                              !wino_any(R, cc, nb, nh, nw, m->down[i].r0.c1);
     _Float16* pool_h = pool_planes ? R.ws.get<_Float16>(2 * pool_el) : nullptr;
@@ -1871,7 +1773,7 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
     float* cat = R.ws.get<float>(cat_el);
     // the concat feeds conv1 (split GEMM: also as f16 planes) and the residual (fp32)
     const bool cat_planes = R.m->prec >= 1 && m->up[i].r0.c1.Bh != nullptr && !R.m->debug && cat_planes_enabled() &&
-                            !(cat_planes_mode() == 2 && (halo_bn(R, u.C, N, sh[si], sw[si], m->up[i].r0.c1, EPI_STATS, true) > 0 ||
+                            !((halo_bn(R, u.C, N, sh[si], sw[si], m->up[i].r0.c1, EPI_STATS, true) > 0 ||
                                                          halo_ms_bn_any(R, u.C, N, sh[si], sw[si], m->up[i].r0.c1))) &&
                             !wino_any(R, u.C, N, sh[si], sw[si], m->up[i].r0.c1);
     _Float16* cat_h = cat_planes ? R.ws.get<_Float16>(2 * cat_el) : nullptr;
@@ -1883,7 +1785,7 @@ static float* unet_trunk(Run& R, const FwdIn& in, int N, int H, int W) {
     GnLoad dly;
     const bool r1_wino = wino_any(R, u.C, N, sh[si], sw[si], m->up[i].r1.c1);
     const bool try_defer = gn_fuse_enabled() && !R.m->debug && R.m->prec >= 1 &&
-                           (r1_wino ? wino_gna_pays(m->up[i].r1.c1, 2)
+                           (r1_wino ? wino_gna_pays(m->up[i].r1.c1, 2, sw[si])
                                     : halo_bn(R, u.C, N, sh[si], sw[si], m->up[i].r1.c1, EPI_STATS, true) > 0);
     float* h0 = resblock(R, m->up[i].r0, plain_src(cat, u.C), SRC_PLAIN, N, sh[si], sw[si], true, nullptr, 0, 0, 0,
                          cat_h, cat_l, m->up[i].r1.c1.Bh != nullptr && !r1_wino, &hp, try_defer ? &dly : nullptr);

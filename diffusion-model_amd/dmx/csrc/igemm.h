@@ -112,10 +112,6 @@ DMX_DEV unsigned tap_mask(int geom, int phase, int taps, int m, int M, int H, in
   return mk;
 }
 
-// DMX_NT_PART (A/B build): split-K partial slabs stored with the non-temporal hint
-#ifndef DMX_NT_PART
-#define DMX_NT_PART 0
-#endif
 DMX_DEV void xcd_tile(int& mt, int& nt, int& z) {
   const int nm = gridDim.x, nn = gridDim.y;
   const int total = nm * nn;
@@ -152,8 +148,7 @@ DMX_DEV void igemm_epilogue(const IgemmParams& p, floatx16 (&acc)[BM / 64][BN / 
         for (int j = 0; j < TN; ++j) {
           const int col = n0 + wn * WN + j * 32 + fr;
           if (m < p.M && col < p.Cout) {
-            if constexpr (DMX_NT_PART) __builtin_nontemporal_store(acc[i][j][r], &dst[(size_t)m * p.Cout + col]);
-            else dst[(size_t)m * p.Cout + col] = acc[i][j][r];
+            dst[(size_t)m * p.Cout + col] = acc[i][j][r];
           }
         }
       }

@@ -512,15 +512,12 @@ __global__ __launch_bounds__(1024) void igemm_halo_cs_kernel(const X3Params P) {
     }
   };
 
-#ifndef DMX_DIAG_CS
-#define DMX_DIAG_CS 0  // diagnostic builds only (wrong results): 1 no MFMAs, 2 no stores, 3 no loads
-#endif
-  if (DMX_DIAG_CS != 3) load_chunk(0);
+  load_chunk(0);
   store_chunk();
   __syncthreads();
   for (int c = 0; c < nch; ++c) {
-    if (DMX_DIAG_CS != 3 && c + 1 < nch) load_chunk(c + 1);  // in flight under this chunk's MFMAs
-    if (DMX_DIAG_CS != 1) compute_chunk();
+    if (c + 1 < nch) load_chunk(c + 1);  // in flight under this chunk's MFMAs
+    compute_chunk();
     if (c + 1 < nch) {
       __syncthreads();  // every wave done reading chunk c
       store_chunk();
@@ -529,7 +526,6 @@ __global__ __launch_bounds__(1024) void igemm_halo_cs_kernel(const X3Params P) {
   }
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[0][0][r] *= P.inv_scale;
-  if (DMX_DIAG_CS == 2 && acc[0][0][0] != 1234.5f) return;
   igemm_epilogue<64, 64, EPI>(p, acc, 0, m0 + (wm >> 1) * 64, n0, wm & 1, wn, fr, fh);
 }
 

@@ -45,51 +45,19 @@
 
 namespace dmx {
 
-// Diagnostic builds only (-DDMX_WDIAG=bits; wrong results, timing decomposition): 1 no MFMAs,
-// 2 no A-fragment arithmetic (LDS reads kept), 4 no GroupNorm / GELU in the halo store, 8 no output
-// stores, 16 the output bytes stored as two contiguous float4 per thread (wrong layout), 32 no LDS
-// round trip in the epilogue (outputs from the wave's own accumulators); chunk loop: 64 no barrier,
-// 128 no U reloads (chunk 0's fragments throughout), 256 no halo global loads, 512 no halo LDS
-// stores, 1024 no A-fragment LDS reads (halo values from registers).
-#ifndef DMX_WDIAG
-#define DMX_WDIAG 0
+#ifndef DMX_WPIPE  // (A/B build) software-pipelined A build, barrier mid-chunk
+#define DMX_WPIPE 1
 #endif
 
-#ifndef DMX_WPRIO  // (A/B build) s_setprio 1 for waves 4-7 over the chunk loop
-#define DMX_WPRIO 0
-#endif
-#ifndef DMX_WBAR2  // (A/B build) a barrier between the halo store and the A build
-#define DMX_WBAR2 0
-#endif
-#ifndef DMX_WSHFL
-#define DMX_WSHFL 0
-#endif
-#ifndef DMX_WHSW  // (A/B build) bank-conflict-free pixel order of the halo stores
-#define DMX_WHSW 1
-#endif
-#ifndef DMX_WEPP
-#define DMX_WEPP 34
-#endif
-
-// Output stores carry the non-temporal hint (DMX_WNT=0 builds plain stores for A/B): the output is
-// streamed to memory instead of sitting dirty in the XCDs' L2s until the end-of-kernel writeback —
-// every Winograd launch 1.4-7 us faster, its consumers (norm / reduce_norm, now reading it from
-// memory) 0.1-1.7 us slower: +1.5-1.7 % per CFG step, 3 / 3 same-box rounds.
-#ifndef DMX_WNT
-#define DMX_WNT 1
-#endif
-#ifndef DMX_WNT_PART  // (A/B build) the hint on EPI_PARTIAL split slabs too (read back at once by the reduce)
-#define DMX_WNT_PART 1
-#endif
-
-// Diagnostic builds only (-DDMX_WSTAMP=1, k_wino.hip's dmx_diag_wino_stamps reads them): wave 0 of
+// Diagnostic builds only (-DDMX_DIAG=1, k_wino.hip's dmx_diag_wino_stamps reads them): wave 0 of
 // every block records s_memtime at kernel start, after the prologue barrier, after the chunk loop
 // and at the end, plus the hardware id (XCC, CU), into g_wstamp[launch slot][block] — timing only,
-// no output value depends on them (MI355X_MICROARCH.md DVFS note 6).
-#ifndef DMX_WSTAMP
-#define DMX_WSTAMP 0
+// no output value depends on them (MI355X_MICROARCH.md DVFS note 6).  (Round 5's timing
+// decompositions — builds without MFMAs, transforms, stores, ... — are recorded in DESIGN §6d / §6e.)
+#ifndef DMX_DIAG
+#define DMX_DIAG 0
 #endif
-#if DMX_WSTAMP
+#if DMX_DIAG
 constexpr int WSTAMP_SLOTS = 32, WSTAMP_BLOCKS = 2048;
 __device__ unsigned long long g_wstamp[WSTAMP_SLOTS * WSTAMP_BLOCKS * 5];
 DMX_DEV void wstamp(int slot, int k) {
@@ -189,8 +157,8 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   // epilogue LDS row pitch: 32 tiles + 2 — with 8-byte stores / reads, 34 cc mod 64 dwords puts
   // the 32 lanes of each ds_read_b64 group on 32 distinct bank pairs (a pitch of 36, needed by
   // 16-byte stores, made every read 2-way conflicted): Winograd launches -2 % in the eager
-  // breakdown (DMX_WEPP=36 builds the old layout)
-  constexpr int EPP = DMX_WEPP;
+  // breakdown
+  constexpr int EPP = 34;
   constexpr int EPF = 16 * 32 * EPP;        // epilogue floats (one 32 x 32 pass, 16 positions)
   constexpr int LDSF = 2 * HBUF + 1024 > EPF ? 2 * HBUF + 1024 : EPF;
   __shared__ __attribute__((aligned(16))) float lds[LDSF];
@@ -229,7 +197,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
     // Plain row-major slots put parity-plane neighbours on the same banks (2-way conflicts on every
     // halo store).
     int hrow, hcol;
-    if constexpr (!DMX_WHSW || RING0) {
+    if constexpr (RING0) {
       hrow = h / HC;
       hcol = h - hrow * HC;
     } else if constexpr (W == 32) {
@@ -290,9 +258,6 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   floatx4 ha[NPI];
   floatx4 hr[GNA == 2 ? NPI : 1];
   auto load_halo = [&](int c) {
-    if constexpr ((DMX_WDIAG & 256) != 0) {
-      if (c > 1) return;
-    }
 #pragma unroll
     for (int k = 0; k < NPI; ++k) {
       const int off = hoff[k] >= 0 ? (hoff[k] + (cbeg + c) * CK) * 4 : kOOB;
@@ -301,9 +266,6 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
     }
   };
   auto store_halo = [&](int buf, int c) {
-    if constexpr ((DMX_WDIAG & 512) != 0) {
-      if (c > 1) return;
-    }
     float* hb = lds + buf * HBUF;
     floatx4 ggam = {0.f, 0.f, 0.f, 0.f}, gbet = {0.f, 0.f, 0.f, 0.f};
     if constexpr (GNA) {  // every piece of this thread holds the same channel quad (512 % 4 == 0)
@@ -314,7 +276,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
 #pragma unroll
     for (int k = 0; k < NPI; ++k) {
       floatx4 v = ha[k];
-      if constexpr (GNA && !(DMX_WDIAG & 4)) {  // GroupNorm (+ residual) + GELU of the raw source; zero padding stays zero
+      if constexpr (GNA) {  // GroupNorm (+ residual) + GELU of the raw source; zero padding stays zero
         const float2 gst = gst_s[SPB == 1 ? 0 : min(hls[k] / SQ, SPB - 1)];  // (the piece's stacked sample)
         v = gn_apply4v(v, gst, ggam, gbet, GNA == 1 ? 1 : 0);
         if constexpr (GNA == 2) {
@@ -340,9 +302,6 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   half8 bh[2][2], bl[2][2];
   int cnext = 0;  // chunk whose fragments load_b(.., -1) fetches
   auto load_b = [&](int q, int n, int c) {
-    if constexpr ((DMX_WDIAG & 128) != 0) {
-      if (c < 0) return;
-    }
     const int cc = c < 0 ? cnext : c;
     bh[q][n] = bload_h8(rUh, voff, ub[q][n] + (cbeg + cc) * 1024);
     if constexpr (!X1) bl[q][n] = bload_h8(rUl, voff, ub[q][n] + (cbeg + cc) * 1024);
@@ -365,7 +324,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
     const int t = 32 * mb + fr, st = t / TPS, tt = t - st * TPS, ty = tt / TW, tx = tt - ty * TW;
     tb[mb] = st * SQ + 2 * ty * 8 * RP + tx * 20 + 8 * fh;
   }
-  half8 ah[2], al[2];  // [position] of the current m tile
+  half8 ah[2][2], al[2][2];  // [m tile][position]
   auto build = [&](int buf, int mb) {
     const float* hb = lds + buf * HBUF + tb[mb];
     unsigned vh[2][4], vl[2][4];
@@ -375,31 +334,10 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
       const int oc[3] = {op, oq, os};
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        floatx4 da, db;
-        if constexpr ((DMX_WDIAG & 1024) != 0) {
-          da = floatx4{hb[0], hb[1], (float)k, (float)h};
-          db = floatx4{hb[2], (float)oc[k], (float)k, (float)h};
-        } else {
-          da = *reinterpret_cast<const floatx4*>(hb + oa + oc[k] + 4 * h);
-          db = *reinterpret_cast<const floatx4*>(hb + ob + oc[k] + 4 * h);
-        }
-        if constexpr (DMX_WDIAG & 2) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) T[k][e] = k == 2 ? db[e] : da[e];
-          continue;
-        }
+        const floatx4 da = *reinterpret_cast<const floatx4*>(hb + oa + oc[k] + 4 * h);
+        const floatx4 db = *reinterpret_cast<const floatx4*>(hb + ob + oc[k] + 4 * h);
 #pragma unroll
         for (int e = 0; e < 4; ++e) T[k][e] = fmaf(db[e], sr, da[e]);
-      }
-      if constexpr (DMX_WDIAG & 2) {
-#pragma unroll
-        for (int e = 0; e < 4; e += 2) {
-          vh[0][2 * h + e / 2] = __builtin_bit_cast(unsigned, T[0][e]) & 0x3bff3bffu;  // (finite f16)
-          vl[0][2 * h + e / 2] = __builtin_bit_cast(unsigned, T[1][e + 1]) & 0x3bff3bffu;
-          vh[1][2 * h + e / 2] = __builtin_bit_cast(unsigned, T[2][e]) & 0x3bff3bffu;
-          vl[1][2 * h + e / 2] = __builtin_bit_cast(unsigned, T[1][e]) & 0x3bff3bffu;
-        }
-        continue;
       }
 #pragma unroll
       for (int e = 0; e < 4; e += 2) {
@@ -416,8 +354,8 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
     }
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      ah[q] = __builtin_bit_cast(half8, (u32x4){vh[q][0], vh[q][1], vh[q][2], vh[q][3]});
-      if constexpr (!X1) al[q] = __builtin_bit_cast(half8, (u32x4){vl[q][0], vl[q][1], vl[q][2], vl[q][3]});
+      ah[mb][q] = __builtin_bit_cast(half8, (u32x4){vh[q][0], vh[q][1], vh[q][2], vh[q][3]});
+      if constexpr (!X1) al[mb][q] = __builtin_bit_cast(half8, (u32x4){vl[q][0], vl[q][1], vl[q][2], vl[q][3]});
     }
   };
 
@@ -471,24 +409,125 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
     for (int q = 0; q < 2; ++q)
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
-        if constexpr (DMX_WDIAG & 1) {
-          asm volatile("" ::"v"(al[q]), "v"(ah[q]), "v"(bh[q][n]), "v"(bl[q][n]));
-        } else {
-          if constexpr (!X1) {
-            acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[q], bh[q][n], acc[q][i][n], 0, 0, 0);
-            acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[q], bl[q][n], acc[q][i][n], 0, 0, 0);
-          }
-          acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[q], bh[q][n], acc[q][i][n], 0, 0, 0);
+        if constexpr (!X1) {
+          acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[i][q], bh[q][n], acc[q][i][n], 0, 0, 0);
+          acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i][q], bl[q][n], acc[q][i][n], 0, 0, 0);
         }
+        acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[i][q], bh[q][n], acc[q][i][n], 0, 0, 0);
         if (reload) {
           load_b(q, n, -1);
           __builtin_amdgcn_sched_barrier(0x0086);
         }
       }
   };
-  if constexpr (DMX_WPRIO) {  // static priority for the second-dispatched half (MI355X_MICROARCH item 4)
-    if (wid >= 4) __builtin_amdgcn_s_setprio(1);
-  }
+  // (GroupNorm-on-load instances keep the plain loop: their halo store's VALU and registers make the
+  // pipelined one spill)
+  if constexpr (DMX_WPIPE && GNA == 0) {
+  // Software-pipelined A build (one barrier per chunk, in the middle).  Iteration c runs m tile 0's
+  // MFMAs beside the build of m tile 1's A fragments (halo buffer c & 1); then, after the barrier
+  // that publishes chunk c + 1's halo, m tile 1's MFMAs beside the build of chunk c + 1's m tile 0
+  // fragments (buffer (c + 1) & 1) and the U reloads — so the matrix pipe never waits for a whole A
+  // build.  Buffer (c + 1) & 1 is stored at the top of iteration c; its previous readers (chunk
+  // c - 1's builds) all precede barrier c - 1, and its readers in iteration c follow barrier c.
+  // The build is cut into pieces (LDS reads of a 4-channel half, its T columns, its V / split), one
+  // piece per MFMA slot; sched_barrier(0) between slots keeps the order as written, so the reads run
+  // ahead of their VALU by three slots and every MFMA has the transform work of its slot beside it.
+  constexpr int NM = X1 ? 4 : 12;  // MFMAs per m tile and chunk
+  floatx4 pda[2][3], pdb[2][3], pT[3];
+  u32x4 pah[2][2], pal[2][2];  // [m tile][position] A fragments (f16 pairs)
+  auto p_read = [&](int buf, int mb, int h) {
+    const float* hb = lds + buf * HBUF + tb[mb];
+    const int oc[3] = {op, oq, os};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      pda[h][k] = *reinterpret_cast<const floatx4*>(hb + oa + oc[k] + 4 * h);
+      pdb[h][k] = *reinterpret_cast<const floatx4*>(hb + ob + oc[k] + 4 * h);
+    }
+  };
+  auto p_T = [&](int h) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pT[k][e] = fmaf(pdb[h][k][e], sr, pda[h][k][e]);
+  };
+  auto p_V = [&](int mb, int h, int e) {  // channels 4h + e, 4h + e + 1
+    const float a0 = pT[0][e] - pT[1][e], a1 = pT[0][e + 1] - pT[1][e + 1];
+    const float b0 = fmaf(pT[2][e], sb, pT[1][e]), b1 = fmaf(pT[2][e + 1], sb, pT[1][e + 1]);
+    const int j = 2 * h + e / 2;
+    if constexpr (X1) {
+      pah[mb][0][j] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){a0, a1}, half2v));
+      pah[mb][1][j] = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){b0, b1}, half2v));
+    } else {
+      unsigned h0, l0, h1, l1;
+      split2u(a0, a1, h0, l0);
+      split2u(b0, b1, h1, l1);
+      pah[mb][0][j] = h0;
+      pal[mb][0][j] = l0;
+      pah[mb][1][j] = h1;
+      pal[mb][1][j] = l1;
+    }
+  };
+  // build piece of slot s (build target m tile mb from buffer buf); -1: none
+  auto p_piece = [&](int s, int buf, int mb) {
+    if constexpr (X1) {
+      if (s == 0) { p_read(buf, mb, 0); p_read(buf, mb, 1); }
+      if (s == 1) { p_T(0); p_V(mb, 0, 0); p_V(mb, 0, 2); }
+      if (s == 2) { p_T(1); p_V(mb, 1, 0); p_V(mb, 1, 2); }
+    } else {
+      if (s == 0) p_read(buf, mb, 0);
+      if (s == 3) { p_T(0); p_read(buf, mb, 1); }
+      if (s == 4) p_V(mb, 0, 0);
+      if (s == 5) p_V(mb, 0, 2);
+      if (s == 6) p_T(1);
+      if (s == 7) p_V(mb, 1, 0);
+      if (s == 8) p_V(mb, 1, 2);
+    }
+  };
+  // MFMA slot s of m tile i: position q, column tile n, product (x3: al*bh, ah*bl, ah*bh)
+  auto p_mfma = [&](int i, int s) {
+    const int pr = X1 ? 2 : s % 3, qn = X1 ? s : s / 3, q = qn >> 1, n = qn & 1;
+    const half8 A = __builtin_bit_cast(half8, pr == 0 ? pal[i][q] : pah[i][q]);
+    const half8 Bf = pr == 1 ? bl[q][n] : bh[q][n];
+    acc[q][i][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A, Bf, acc[q][i][n], 0, 0, 0);
+  };
+  // prologue build: chunk 0's m tile 0 (buffer 0, published by the prologue barrier)
+  p_read(0, 0, 0);
+  p_T(0);
+  p_read(0, 0, 1);
+  p_V(0, 0, 0);
+  p_V(0, 0, 2);
+  p_T(1);
+  p_V(0, 1, 0);
+  p_V(0, 1, 2);
+  constexpr bool LATE = GNA == 2 || (W != 32 && GNA == 1);  // (register pressure: after the barrier)
+  auto iter = [&](int c, auto last) {
+    store_halo((c + 1) & 1, min(c + 1, nch - 1));  // c + 1 = nch: an unused store of the last chunk
+    if constexpr (!LATE) load_halo(min(c + 2, nch - 1));
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int sl = 0; sl < NM; ++sl) {  // phase X: m tile 0 (A built last phase) | build m tile 1
+      p_mfma(0, sl);
+      p_piece(sl, c & 1, 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __syncthreads();
+    if constexpr (LATE) load_halo(min(c + 2, nch - 1));
+    cnext = min(c + 1, nch - 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int sl = 0; sl < NM; ++sl) {  // phase Y: m tile 1 | build chunk c + 1's m tile 0, U reloads
+      p_mfma(1, sl);
+      if constexpr (!decltype(last)::value) p_piece(sl, (c + 1) & 1, 0);
+      if (X1 || sl % 3 == 2) {
+        const int qn = X1 ? sl : sl / 3;
+        load_b(qn >> 1, qn & 1, -1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  for (int c = 0; c < nch - 1; ++c) iter(c, std::false_type{});
+  iter(nch - 1, std::true_type{});
+  } else {
   for (int c = 0; c < nch; ++c) {
     store_halo((c + 1) & 1, min(c + 1, nch - 1));  // c + 1 = nch: an unused store of the last chunk
     // (No barrier here: buffer (c + 1) & 1 was last read by chunk c - 1's builds, which the previous
@@ -496,8 +535,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
     // buffer.  An earlier build with the GroupNorm affine in an LDS table was nondeterministic
     // without a barrier here (tools/det_check.py); with the affine read from global memory the
     // barrier is not needed — 0 of 9 repeats and 0 of 36 concurrent-process steps differ — and
-    // dropping it is +1.7-2.2 % per CFG step, 3 / 3 same-box rounds.  DMX_WBAR2=1 builds it back.)
-    if constexpr (DMX_WBAR2) __syncthreads();
+    // dropping it is +1.7-2.2 % per CFG step, 3 / 3 same-box rounds.)
     constexpr bool LATE = GNA == 2 || (W != 32 && GNA == 1);  // (register pressure: after m tile 0)
     if constexpr (!LATE) {
       load_halo(min(c + 2, nch - 1));
@@ -512,7 +550,8 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
     build(c & 1, 1);
     cnext = min(c + 1, nch - 1);
     mfmas(1, true);
-    if constexpr ((DMX_WDIAG & 64) == 0) __syncthreads();
+    __syncthreads();
+  }
   }
 
   // ---- epilogue: Aᵀ M A per tile, four passes of 32 tiles x 32 channels through LDS
@@ -528,29 +567,20 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
     for (int n = 0; n < 2; ++n) {
       // positions -> LDS [xi][channel][tile] (rows of a lane's accumulator are 4 consecutive tiles)
 #pragma unroll
-      for (int q = 0; q < ((DMX_WDIAG & 32) ? 0 : 2); ++q)
+      for (int q = 0; q < 2; ++q)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           floatx4 v;
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = acc[q][mb][n][4 * k + e] * P.inv_scale;
           float* e = &lds[((xi0 + q) * 32 + fr) * EPP + 8 * k + 4 * fh];
-          if constexpr (EPP % 4 == 0) {
-            *reinterpret_cast<floatx4*>(e) = v;
-          } else {
-            *reinterpret_cast<f32x2*>(e) = f32x2{v[0], v[1]};
-            *reinterpret_cast<f32x2*>(e + 2) = f32x2{v[2], v[3]};
-          }
+          *reinterpret_cast<f32x2*>(e) = f32x2{v[0], v[1]};
+          *reinterpret_cast<f32x2*>(e + 2) = f32x2{v[2], v[3]};
         }
       __syncthreads();
       float m[16][2];
 #pragma unroll
       for (int xi = 0; xi < 16; ++xi) {
-        if constexpr ((DMX_WDIAG & 32) != 0) {  // diagnostic: no LDS round trip (wrong values)
-          m[xi][0] = acc[xi & 1][mb][n][xi >> 1];
-          m[xi][1] = acc[(xi >> 1) & 1][mb][n][(xi + 3) & 15];
-          continue;
-        }
         const f32x2 v = *reinterpret_cast<const f32x2*>(&lds[(xi * 32 + cc) * EPP + 2 * tp]);
         m[xi][0] = v.x;
         m[xi][1] = v.y;
@@ -560,7 +590,6 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
       const float bias = (EPI == EPI_STATS && p.bias != nullptr) ? p.bias[col] : 0.f;
       float* dst = EPI == EPI_PARTIAL ? p.partial + (size_t)bz * p.M * p.Cout : p.out;
       float s1 = 0.f, s2 = 0.f;
-      float ys[8];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         float z[4][2];
@@ -577,37 +606,19 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
             const float y = (r == 0 ? (z[0][s] + z[1][s]) + z[2][s] : (z[1][s] - z[2][s]) - z[3][s]) + bias;
             const int oy = y0 + 2 * ty + r, ox = 2 * tx + s;
             const bool in = oy < p.H && ox < WA;
-            if (!(DMX_WDIAG & 24) && nsmp + st < nsamp && in) {
-              float* a = &dst[(((size_t)(nsmp + st) * p.H + oy) * WA + ox) * p.Cout + col];
-              if constexpr (DMX_WNT && (EPI == EPI_STATS || DMX_WNT_PART)) __builtin_nontemporal_store(y, a);
-              else *a = y;
-            }
-            ys[4 * e + 2 * r + s] = y;
+            // non-temporal: the output streams to memory instead of sitting dirty in the XCDs' L2s
+            // until the end-of-kernel writeback (+1.5-1.7 % per CFG step, split slabs +0.8 %)
+            if (nsmp + st < nsamp && in)
+              __builtin_nontemporal_store(y, &dst[(((size_t)(nsmp + st) * p.H + oy) * WA + ox) * p.Cout + col]);
             const float yv = in ? y : 0.f;
             s1 += yv;
             s2 += yv * yv;
           }
       }
-      if constexpr ((DMX_WDIAG & 16) != 0) {  // same bytes as two contiguous float4 per thread (wrong layout)
-        const size_t blin = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
-        if ((blin + 1) * 16384 <= (size_t)p.M * p.Cout) {
-          float* q = dst + blin * 16384 + (2 * mb + n) * 4096 + tid * 8;
-          *reinterpret_cast<floatx4*>(q) = floatx4{ys[0], ys[1], ys[2], ys[3]};
-          *reinterpret_cast<floatx4*>(q + 4) = floatx4{ys[4], ys[5], ys[6], ys[7]};
-        }
-      }
       // partial of 4 tiles (16 pixels) x 32 channels = this wave's 64 lanes
       if constexpr (EPI == EPI_STATS) {  // (DPP / permlane: no LDS round trips in the epilogue)
-#if DMX_WSHFL  // (A/B build: the ds_bpermute tree)
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          s1 += __shfl_xor(s1, o, 64);
-          s2 += __shfl_xor(s2, o, 64);
-        }
-#else
         s1 = wave_sum_dpp(s1);
         s2 = wave_sum_dpp(s2);
-#endif
       }
       if (EPI == EPI_STATS && lane == 0) {  // the wave's 4 tiles: one tile row of one sample
         const int t = 32 * mb + 4 * wid, st = t / TPS, g = (tile0 + t - st * TPS) / 4;

@@ -16,10 +16,6 @@
 #include "common.h"
 #include "igemm.h"
 
-#ifndef DMX_DIAG_GEMM
-#define DMX_DIAG_GEMM 0
-#endif
-
 namespace dmx {
 
 
@@ -50,7 +46,7 @@ struct X3Params {
   const _Float16* Uh;
   const _Float16* Ul;
   unsigned u_bytes;          // bytes of one U plane (16 * Cout * Cin f16)
-  int dslot;                 // diagnostic builds (DMX_WSTAMP): stamp slot of this launch, else unused
+  int dslot;                 // diagnostic builds (DMX_DIAG): stamp slot of this launch, else unused
 };
 
 
@@ -69,14 +65,9 @@ DMX_DEV floatx4 bload_f4(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   return __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 
-// DMX_NT_ATT (A/B build): attention outputs stored with the non-temporal hint
-#ifndef DMX_NT_ATT
-#define DMX_NT_ATT 0
-#endif
-DMX_DEV void att_st4(float* a, floatx4 v) {
-  if constexpr (DMX_NT_ATT) __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(a));
-  else *reinterpret_cast<floatx4*>(a) = v;
-}
+// (attention outputs: plain stores — the token kernel reads them back from L2; the non-temporal
+// hint measured neutral, round 4)
+DMX_DEV void att_st4(float* a, floatx4 v) { *reinterpret_cast<floatx4*>(a) = v; }
 
 // hi/lo split of two fp32 values as packed f16 pairs (common.h split2u: 3 VALU ops per pair).
 DMX_DEV void split2(f32x2 v, unsigned& h, unsigned& l) { split2u(v.x, v.y, h, l); }
@@ -144,7 +135,6 @@ __global__ __launch_bounds__(64 * NW) void igemm_x3_kernel(const X3Params P) {
     lc = k - ltap * C;
   };
   const float* __restrict__ asrc = p.src.src0;
-#ifndef DMX_NO_BUFLOAD
   // Buffer-resource addressing: 32-bit byte offsets; a masked piece gets an out-of-range offset
   // and reads zeros (no 64-bit address math / selects per piece); B offsets are per-thread
   // constants plus a wave-uniform K-tile offset.
@@ -155,7 +145,6 @@ __global__ __launch_bounds__(64 * NW) void igemm_x3_kernel(const X3Params P) {
   int boffs[BP];
 #pragma unroll
   for (int i = 0; i < BP; ++i) boffs[i] = ((n0 + rb + i * BRS) * p.Kpad + qb * 8) * 2;
-#endif
   auto load_tile = [&](int kt, int st) {  // st: register stage (compile-time constant at every call)
     int ddy, ddx;
     tap_offset(p.geom, phase, ltap, ddy, ddx);
@@ -173,7 +162,6 @@ __global__ __launch_bounds__(64 * NW) void igemm_x3_kernel(const X3Params P) {
       // compute() (a select on the data forced a vmcnt wait before the MFMAs).
       const bool ok = (tmask[i] >> tap) & 1u;
       const int off = (rpix[i] + delta) * C + c;
-#ifndef DMX_NO_BUFLOAD
       const int boff_a = ok ? off * AES : kOOB;
       if constexpr (SPLIT_A) {
         rah[st][i] = bload_h8(rAh, boff_a, 0);
@@ -181,29 +169,11 @@ __global__ __launch_bounds__(64 * NW) void igemm_x3_kernel(const X3Params P) {
       } else {
         ra4[st][i] = bload_f4(rAh, boff_a, 0);
       }
-#else
-      if constexpr (SPLIT_A) {
-        const _Float16* ph = ok ? P.Ash + off : reinterpret_cast<const _Float16*>(g_zero16);
-        rah[st][i] = *reinterpret_cast<const half8*>(ph);
-        if constexpr (!X1) {
-          const _Float16* pl = ok ? P.Asl + off : reinterpret_cast<const _Float16*>(g_zero16);
-          ral[st][i] = *reinterpret_cast<const half8*>(pl);
-        }
-      } else {
-        ra4[st][i] = ld4(ok ? asrc + off : g_zero16);
-      }
-#endif
     }
 #pragma unroll
     for (int i = 0; i < BP; ++i) {
-#ifndef DMX_NO_BUFLOAD
       rbh[st][i] = bload_h8(rBh, boffs[i], kt * BK * 2);
       if constexpr (!X1) rbl[st][i] = bload_h8(rBl, boffs[i], kt * BK * 2);
-#else
-      const size_t o = (size_t)(n0 + rb + i * BRS) * p.Kpad + kt * BK + qb * 8;
-      rbh[st][i] = *reinterpret_cast<const half8*>(Bh + o);
-      if constexpr (!X1) rbl[st][i] = *reinterpret_cast<const half8*>(Bl + o);
-#endif
     }
   };
   auto store_tile = [&](int buf, int st) {
@@ -321,13 +291,8 @@ __global__ __launch_bounds__(64 * NW) void igemm_x3_kernel(const X3Params P) {
     for (int kt = 0; kt < nK; ++kt) {
       store_tile(0, 0);
       __syncthreads();
-#if DMX_DIAG_GEMM == 2  // diagnostic build only (wrong results): no global loads after the first tile
-      if (false)
-#endif
       if (kt + 1 < nK) load_tile(kbeg + kt + 1, 0);  // in flight during the MFMAs
-#if DMX_DIAG_GEMM != 1  // diagnostic build only (wrong results): no MFMAs / fragment reads
       compute(0);
-#endif
       __syncthreads();
     }
   }
@@ -448,9 +413,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     __syncthreads();  // previous chunk fully consumed
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
-#ifdef DMX_DIAG_ATT_NOSTAGE  // diagnostic build only: wrong results, measures the staging cost
-      if (c0 > 0) break;
-#endif
       const int i = tid + 256 * it, key = i / (D / 4), d4 = (i % (D / 4)) * 4;
       const bool kvalid = c0 + key < L;  // keys past L: zero K / V (their scores are masked)
       const floatx4 z = {0.f, 0.f, 0.f, 0.f};
@@ -639,10 +601,8 @@ DMX_DEV floatx16 mfma_untied(half8 a, half8 b, floatx16 c) {
   return d;
 }
 
-// stag > 0: the waves with (wid >> 2) odd (one of each SIMD's wave pairs) start stag x 64 cycles
-// late, so co-resident waves sit in different phases of the QK^T / softmax / PV sequence.
 template <int NW, int X1 = 0>
-__global__ __launch_bounds__(NW * 64) void attention16_kernel(const float* qkv, float* out, int L, int C, int stag) {
+__global__ __launch_bounds__(NW * 64) void attention16_kernel(const float* qkv, float* out, int L, int C) {
   constexpr int D = 16;
   extern __shared__ __attribute__((aligned(16))) _Float16 att_lds[];
   const int Lp = att16_lp(L), VS = Lp + 4;
@@ -706,8 +666,6 @@ __global__ __launch_bounds__(NW * 64) void attention16_kernel(const float* qkv, 
   const _Float16* vrh = Vh + (fr < 16 ? fr : fr == 16 ? 16 : 17) * VS;  // this lane's V^T row (hi)
   const _Float16* vrl = Vl + (fr < 16 ? fr : 16) * VS;                  // (lo)
   const int nqt = (L + 31) / 32;
-  if ((wid >> 2) & 1)
-    for (int i = 0; i < stag; ++i) __builtin_amdgcn_s_sleep(1);
   for (int qt = wid; qt < nqt; qt += NW) {
     const int q = qt * 32 + fr;
     half8 qh, ql;
@@ -827,240 +785,6 @@ __global__ __launch_bounds__(NW * 64) void attention16_kernel(const float* qkv, 
         att_st4(out + ((size_t)n * L + q) * C + hd * D + d, v);
       }
     }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// D = 16 attention core, PV on v_mfma_f32_16x16x32_f16 (attention16pv_kernel; sa5 / sa6).  As
-// attention16_kernel (S^T = K Q^T on 32x32x16 MFMAs, the same lazily rescaled log2-domain softmax),
-// but O^T += V^T P^T runs on 16 x 16 x 32 tiles: V^T is 16 rows (no ones / zero padding rows), so the
-// product does none of attention16_kernel's padded half — 6 instead of 6 MFMAs of twice the cycles
-// per 32 keys in x3 mode.  The B operands (P^T, 32 keys x 16 queries) come out of the S^T
-// accumulator by v_permlane16_swap: with X / Y the packed P of the lane's two 8-key halves (keys
-// {0-3, 8-11} + 4h and {16-19, 24-27} + 4h of query fr), swapping the odd 16-lane rows of X with the
-// even rows of Y leaves X holding queries 0-15 and Y queries 16-31, each lane group g = lane >> 4 with
-// keys {0-3,8-11}, {16-19,24-27}, {4-7,12-15}, {20-23,28-31} (+ c0) — a disjoint cover, matched by the
-// V^T fragment reads.  The softmax denominator is summed in fp32 on the VALU (16 adds per chunk).
-// LDS: K hi / lo [Lp][16] with the 8-dim halves XOR-swizzled by row bit 3; V^T hi / lo 16 rows, row d
-// at dword d * R + 2 (d & 3) + 16 (d >> 2) (R = a multiple of 64 dwords), which puts the 64 lanes of
-// every ds_read_b64 of a fragment on 64 distinct banks.
-// ---------------------------------------------------------------------------
-__host__ __device__ inline int att16pv_rdw(int L) { return (att16_lp(L) / 2 + 63) / 64 * 64 + 64; }  // dwords / V^T row
-__host__ __device__ inline size_t att16pv_lds_bytes(int L, int x1) {
-  const size_t lp = (size_t)att16_lp(L), vb = (size_t)16 * att16pv_rdw(L) * 4;
-  return (x1 ? 1 : 2) * (lp * 16 * 2 + vb);
-}
-
-template <int NW, int X1 = 0>
-__global__ __launch_bounds__(NW * 64) void attention16pv_kernel(const float* qkv, float* out, int L, int C) {
-  constexpr int D = 16;
-  extern __shared__ __attribute__((aligned(16))) _Float16 att_lds[];
-  const int Lp = att16_lp(L), RH = 2 * att16pv_rdw(L);  // V^T row stride in halves
-  _Float16* Kh = att_lds;
-  _Float16* Kl = Kh + Lp * D;
-  _Float16* Vh = Kl + (X1 ? 0 : Lp * D);
-  _Float16* Vl = Vh + 16 * RH;
-  auto vrow = [&](int d) { return d * RH + 4 * (d & 3) + 32 * (d >> 2); };  // halves
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int hd = blockIdx.y, n = blockIdx.z;
-  const int fr = lane & 31, fh = lane >> 5;
-  const size_t rs = (size_t)3 * C;
-  const float* base = qkv + (size_t)n * L * rs + hd * D;
-
-  for (int u = tid; u < Lp; u += NW * 64) {  // a unit = 4 consecutive keys x 4 dims
-    const int k0 = (u >> 2) * 4, d4 = (u & 3) * 4;
-    floatx4 kv[4], vv[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const bool ok = k0 + j < L;
-      const float* r = base + (size_t)(ok ? k0 + j : 0) * rs + d4;
-      kv[j] = ok ? ld4(r + C) : floatx4{0.f, 0.f, 0.f, 0.f};
-      vv[j] = ok ? ld4(r + 2 * C) : floatx4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      half4 h, l;
-      const int kd = (((d4 >> 3) ^ (((k0 + j) >> 3) & 1)) << 3) | (d4 & 7);
-      if constexpr (X1) {
-        h = __builtin_convertvector(kv[j], half4);
-      } else {
-        split4(kv[j], h, l);
-        *reinterpret_cast<half4*>(&Kl[(k0 + j) * D + kd]) = l;
-      }
-      *reinterpret_cast<half4*>(&Kh[(k0 + j) * D + kd]) = h;
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const floatx4 t = {vv[0][e], vv[1][e], vv[2][e], vv[3][e]};
-      half4 h, l;
-      if constexpr (X1) {
-        h = __builtin_convertvector(t, half4);
-      } else {
-        split4(t, h, l);
-        *reinterpret_cast<half4*>(&Vl[vrow(d4 + e) + k0]) = l;
-      }
-      *reinterpret_cast<half4*>(&Vh[vrow(d4 + e) + k0]) = h;
-    }
-  }
-  __syncthreads();
-
-  const float qscale = 1.4426950408889634f / sqrtf((float)D);
-  const int g = lane >> 4, dv = lane & 15;
-  const int kg = (g & 1) * 16 + (g >> 1) * 4;  // this lane group's first key of the chunk
-  const _Float16* vrh = Vh + vrow(dv) + kg;
-  const _Float16* vrl = Vl + vrow(dv) + kg;
-  const int nqt = (L + 31) / 32;
-  for (int qt = wid; qt < nqt; qt += NW) {
-    const int q = qt * 32 + fr;
-    half8 qh, ql;
-    {
-      floatx4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
-      if (q < L) {
-        const float* r = base + (size_t)q * rs + 8 * fh;
-        a = ld4(r);
-        b = ld4(r + 4);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float va = a[j] * qscale, vb = b[j] * qscale;
-        const _Float16 ha = (_Float16)va, hb = (_Float16)vb;
-        qh[j] = ha;
-        ql[j] = (_Float16)(va - (float)ha);
-        qh[j + 4] = hb;
-        ql[j + 4] = (_Float16)(vb - (float)hb);
-      }
-    }
-    constexpr float TAU = 8.f;
-    floatx4 o0 = {0.f, 0.f, 0.f, 0.f}, o1 = {0.f, 0.f, 0.f, 0.f};  // O^T: queries 0-15 / 16-31
-    floatx16 negm;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) negm[r] = 0.f;
-    float mref = 0.f, lsum = 0.f;  // lsum: this lane's 16 keys per chunk, query fr
-    for (int c0 = 0; c0 < L; c0 += 32) {
-      floatx16 sc;
-      {
-        const int krow = (c0 + fr) * D + 8 * (fh ^ ((fr >> 3) & 1));
-        const half8 kh = *reinterpret_cast<const half8*>(&Kh[krow]);
-        if constexpr (!X1) {
-          const half8 kl = *reinterpret_cast<const half8*>(&Kl[krow]);
-          sc = mfma_untied(kl, qh, negm);
-          sc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, ql, sc, 0, 0, 0);
-          sc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kh, qh, sc, 0, 0, 0);
-        } else {
-          sc = mfma_untied(kh, qh, negm);
-        }
-      }
-      const int nvalid = L - c0;
-      if (nvalid < 32) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if ((r & 3) + 8 * (r >> 2) + 4 * fh >= nvalid) sc[r] = -INFINITY;
-      }
-      float mx = sc[0];
-#pragma unroll
-      for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sc[r]);
-      mx = max_halves(mx);
-      // The reference moves per query (lane fr <-> query fr here), but O^T's lanes hold queries
-      // lane & 15 / 16 + (lane & 15): the per-query factors reach them by one v_permlane16_swap
-      // (rows 0 / 2 -> o0's lanes, rows 1 / 3 -> o1's), so the rescale runs wave-uniformly.
-      const bool mv = c0 == 0 || mx > TAU;
-      if (__builtin_amdgcn_ballot_w64(mv) != 0) {
-        const float ms = mv ? mx : 0.f;
-        const float alpha = mv ? __builtin_amdgcn_exp2f(-mx) : 1.f;
-        const unsigned ua = __builtin_bit_cast(unsigned, alpha);
-        const auto ra = __builtin_amdgcn_permlane16_swap(ua, ua, false, false);
-        const float a0 = __builtin_bit_cast(float, (unsigned)ra[0]), a1 = __builtin_bit_cast(float, (unsigned)ra[1]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          o0[r] *= a0;
-          o1[r] *= a1;
-        }
-        lsum *= alpha;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sc[r] -= ms;
-        mref += ms;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) negm[r] = -mref;
-      }
-      // P = exp2(S^T - mref); X = keys {0-3,8-11}+4h (regs 0-7), Y = {16-19,24-27}+4h (regs 8-15)
-      unsigned xh[4], xl[4], yh[4], yl[4];
-      float ps = 0.f;
-#pragma unroll
-      for (int jp = 0; jp < 8; ++jp) {
-        f32x2 v;
-        v.x = __builtin_amdgcn_exp2f(sc[2 * jp]);
-        v.y = __builtin_amdgcn_exp2f(sc[2 * jp + 1]);
-        ps += v.x + v.y;
-        unsigned h, l;
-        if constexpr (X1) {
-          h = __builtin_bit_cast(unsigned, __builtin_convertvector(v, half2v));
-          l = 0u;
-        } else {
-          split2(v, h, l);
-        }
-        if (jp < 4) {
-          xh[jp] = h;
-          xl[jp] = l;
-        } else {
-          yh[jp - 4] = h;
-          yl[jp - 4] = l;
-        }
-      }
-      lsum += ps;
-      // odd 16-lane rows of X <-> even rows of Y: X -> B operand of queries 0-15, Y -> 16-31
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const auto rh = __builtin_amdgcn_permlane16_swap(xh[j], yh[j], false, false);
-        xh[j] = rh[0];
-        yh[j] = rh[1];
-        if constexpr (!X1) {
-          const auto rl = __builtin_amdgcn_permlane16_swap(xl[j], yl[j], false, false);
-          xl[j] = rl[0];
-          yl[j] = rl[1];
-        }
-      }
-      const half8 b0h = __builtin_bit_cast(half8, (u32x4){xh[0], xh[1], xh[2], xh[3]});
-      const half8 b1h = __builtin_bit_cast(half8, (u32x4){yh[0], yh[1], yh[2], yh[3]});
-      half8 vh;
-      {
-        const half4 a0 = *reinterpret_cast<const half4*>(vrh + c0);
-        const half4 a1 = *reinterpret_cast<const half4*>(vrh + c0 + 8);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          vh[j] = a0[j];
-          vh[j + 4] = a1[j];
-        }
-      }
-      if constexpr (!X1) {
-        half8 vl;
-        const half4 c0l = *reinterpret_cast<const half4*>(vrl + c0);
-        const half4 c1l = *reinterpret_cast<const half4*>(vrl + c0 + 8);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          vl[j] = c0l[j];
-          vl[j + 4] = c1l[j];
-        }
-        const half8 b0l = __builtin_bit_cast(half8, (u32x4){xl[0], xl[1], xl[2], xl[3]});
-        const half8 b1l = __builtin_bit_cast(half8, (u32x4){yl[0], yl[1], yl[2], yl[3]});
-        o0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(vl, b0h, o0, 0, 0, 0);
-        o1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(vl, b1h, o1, 0, 0, 0);
-        o0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, b0l, o0, 0, 0, 0);
-        o1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, b1l, o1, 0, 0, 0);
-      }
-      o0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, b0h, o0, 0, 0, 0);
-      o1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, b1h, o1, 0, 0, 0);
-    }
-    // denominator of query fr: this lane's and its lane ^ 32 partner's key halves
-    {
-      const unsigned u = __builtin_bit_cast(unsigned, lsum);
-      const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-      lsum = __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
-    }
-    // O^T lane layout: query (lane & 15) (+16 for o1), dims 4 g .. 4 g + 3
-    const float inv0 = 1.0f / __shfl(lsum, lane & 15, 64), inv1 = 1.0f / __shfl(lsum, 16 + (lane & 15), 64);
-    const int q0 = qt * 32 + (lane & 15), q1 = q0 + 16;
-    if (q0 < L) att_st4(out + ((size_t)n * L + q0) * C + hd * D + 4 * g, o0 * inv0);
-    if (q1 < L) att_st4(out + ((size_t)n * L + q1) * C + hd * D + 4 * g, o1 * inv1);
   }
 }
 

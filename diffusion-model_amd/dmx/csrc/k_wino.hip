@@ -8,7 +8,7 @@
 
 namespace dmx {
 
-#if DMX_WSTAMP
+#if DMX_DIAG
 static int g_wstamp_next = 0;  // stamp slot of the next Winograd launch (reset by dmx_diag_wino_stamps)
 #endif
 
@@ -32,7 +32,7 @@ static void by_w(int w, int gna, const X3Params& p, dim3 grid, hipStream_t st) {
 
 void launch_wino(int epi, int w, int gna, int x1, const X3Params& p0, dim3 grid, hipStream_t st) {
   X3Params p = p0;
-#if DMX_WSTAMP
+#if DMX_DIAG
   p.dslot = g_wstamp_next++;
 #else
   p.dslot = -1;
@@ -54,10 +54,10 @@ void launch_wino_pack(const float* B, int kpad, int cin, int cout, float scale, 
 
 }  // namespace dmx
 
-// Diagnostic (DMX_WSTAMP builds): copy the Winograd stamp table (slots x 2048 blocks x {t0, t1, t2,
+// Diagnostic (DMX_DIAG builds): copy the Winograd stamp table (slots x 2048 blocks x {t0, t1, t2,
 // t3, hw id}) to the host; returns the number of uint64 copied, 0 in regular builds.
 extern "C" int dmx_diag_wino_stamps(unsigned long long* host, int cap) {
-#if DMX_WSTAMP
+#if DMX_DIAG
   if (host == nullptr) {  // reset: the next launch stamps into slot 0, the table is cleared
     dmx::g_wstamp_next = 0;
     static const std::vector<unsigned long long> zeros(sizeof(dmx::g_wstamp) / 8, 0ull);

@@ -6,13 +6,12 @@ namespace dmx {
 template <int BM, int BN, int SA, int X1>
 static void go(const X3Params& p, dim3 grid, hipStream_t st) {
   if constexpr (BN == 128) {  // 8 waves: 2 x 4 waves of (BM/2) x 32
-    if (x3_waves() == 8 || (x3_waves() == 0 && BM == 128)) {
+    if (BM == 128) {
       igemm_x3_kernel<BM, BN, EPI_STATS, 64, 1, SA, X1, 8><<<grid, 512, 0, st>>>(p);
       return;
     }
   }
-  if (x3_prefetch() == 2) igemm_x3_kernel<BM, BN, EPI_STATS, 64, 1, SA, X1, 4, 2><<<grid, 256, 0, st>>>(p);
-  else igemm_x3_kernel<BM, BN, EPI_STATS, 64, 1, SA, X1><<<grid, 256, 0, st>>>(p);
+  igemm_x3_kernel<BM, BN, EPI_STATS, 64, 1, SA, X1><<<grid, 256, 0, st>>>(p);
 }
 
 template <int SA, int X1>

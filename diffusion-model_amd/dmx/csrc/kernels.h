@@ -273,14 +273,9 @@ struct NormParams {
   _Float16* out_h; _Float16* out_l;  // optional fp16 hi/lo planes (split-precision GEMM operand)
 };
 
-// DMX_NT_NORM (A/B build): norm_kernel / prep_kernel outputs stored with the non-temporal hint
-#ifndef DMX_NT_NORM
-#define DMX_NT_NORM 0
-#endif
-DMX_DEV void st4(float* a, floatx4 v) {
-  if constexpr (DMX_NT_NORM) __builtin_nontemporal_store(v, reinterpret_cast<floatx4*>(a));
-  else *reinterpret_cast<floatx4*>(a) = v;
-}
+// norm_kernel / prep_kernel outputs: plain stores (their consumers read them back from L2; the
+// non-temporal hint measured -0.9 %, round 4)
+DMX_DEV void st4(float* a, floatx4 v) { *reinterpret_cast<floatx4*>(a) = v; }
 static __global__ __launch_bounds__(256) void norm_kernel(const NormParams p) {
   const int n = blockIdx.y, tid = threadIdx.x;
   const int ns = p.n_src > 0 ? n % p.n_src : n;  // source sample (CFG-shared trunk prefix)

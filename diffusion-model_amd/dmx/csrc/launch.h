@@ -15,16 +15,8 @@ namespace dmx {
 // x1 = config-4 fp16 arithmetic.  k_x3_stats.hip (EPI_STATS), k_x3_part.hip (EPI_PARTIAL),
 // k_x3_epi.hip (EPI_BIAS / EPI_BIAS_GELU / EPI_BIAS_RES).
 void launch_x3_stats(int bm, int bn, int sa, int x1, const X3Params& p, dim3 grid, hipStream_t st);
-// waves per block of the EPI_STATS / EPI_PARTIAL instances: 0 (default) 8 for 128 x 128 tiles
-// (up1.0: -3 %, same-box A/B) and 4 otherwise (the 64 x 128 split-K tiles at 4x4 / 8x8 are at
-// parity or slower with 8); 4 or 8 force one (DMX_X3_WAVES).
-inline int x3_waves() {
-  static const int v = [] {
-    const char* e = std::getenv("DMX_X3_WAVES");
-    return e == nullptr ? 0 : std::atoi(e);
-  }();
-  return v;
-}
+// (EPI_STATS / EPI_PARTIAL instances: 8-wave blocks for 128 x 128 tiles — up1.0 -3 %, same-box A/B —
+// and 4 waves otherwise; the 64 x 128 split-K tiles at 4x4 / 8x8 are at parity or slower with 8.)
 void launch_x3_partial(int bm, int bn, int sa, int x1, const X3Params& p, dim3 grid, hipStream_t st);
 void launch_x3_epi(int epi, int bm, int bn, int sa, int x1, const X3Params& p, dim3 grid, hipStream_t st);
 // 512-thread ping-pong split-precision GEMM (igemm_pp.h), EPI_STATS, 256 x bn tiles.
@@ -49,14 +41,6 @@ void launch_wino(int epi, int w, int gna, int x1, const X3Params& p, dim3 grid, 
 // U = G g Gᵀ of a packed fp32 3x3 weight ([npad][kpad], k = tap * cin + c), scaled, split, fragment order
 void launch_wino_pack(const float* B, int kpad, int cin, int cout, float scale, _Float16* uh, _Float16* ul,
                       hipStream_t st);
-// register-stage depth of the 4-wave EPI_STATS / EPI_PARTIAL instances (1 or 2; DMX_X3_PF)
-inline int x3_prefetch() {
-  static const int v = [] {
-    const char* e = std::getenv("DMX_X3_PF");
-    return e == nullptr ? 1 : std::atoi(e);
-  }();
-  return v;
-}
 // exact-fp32 MFMA implicit GEMM (igemm.h), k_f32.hip.
 void launch_f32(int src_mode, int epi, int bm, int bn, const IgemmParams& p, dim3 grid, hipStream_t st);
 // attention cores (k_attn.hip): split-precision (D, waves-per-EU hint, x1) and exact fp32 (D, QT).

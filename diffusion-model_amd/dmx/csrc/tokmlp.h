@@ -21,11 +21,9 @@
 #include "common.h"
 #include "igemm_x3.h"
 
-#ifndef DMX_TOK_PD
-#define DMX_TOK_PD 8  // k16 steps of B fragments in flight in tok_gemm (L2 latency cover)
-#endif
-
 namespace dmx {
+
+constexpr int TOK_PD = 8;  // k16 steps of B fragments in flight in tok_gemm (L2 latency cover)
 
 struct TokW {                 // one Linear in the x3 B layout
   const _Float16* h;          // [Npad][Kpad] hi (scaled by 1/inv_scale)
@@ -177,7 +175,7 @@ DMX_DEV void tok_rows(const float* src, int ld, int m0, int M, const float* g, c
 // the GEMM's A operand exists (under the LayerNorm / epilogue phases and their barriers), so the
 // L2 round trip of the weights is off the critical path; tok_gemm_primed consumes them and keeps
 // PD steps in flight (rolling register prefetch).
-template <int C, int NT, int PDM = DMX_TOK_PD>
+template <int C, int NT, int PDM = TOK_PD>
 struct TokB {
   static constexpr int S = C / 16, PD = S < PDM ? S : PDM;
   half8 h[PD][NT], l[PD][NT];
@@ -208,7 +206,7 @@ DMX_DEV void tok_loadb(const TokBPtr& p, int s, half8* h, half8* l) {
     if constexpr (!X1) l[j] = *reinterpret_cast<const half8*>(p.wl + j * p.jstride + p.sstride * s);
   }
 }
-template <int C, int NT, int X1 = 0, int PDM = DMX_TOK_PD>
+template <int C, int NT, int X1 = 0, int PDM = TOK_PD>
 DMX_DEV void tok_prime(const TokW& w, int nw, int fr, int fh, TokB<C, NT, PDM>& b) {
   const TokBPtr p = tok_bptr(w, nw, fr, fh);
 #pragma unroll
@@ -217,7 +215,7 @@ DMX_DEV void tok_prime(const TokW& w, int nw, int fr, int fh, TokB<C, NT, PDM>& 
 
 // acc[j] = A[arow0 .. +32][0, C) . W[nw + 32j .. +32][0, C)^T  (x3 sum, still scaled by 2^e),
 // B fragments primed by tok_prime (same w, nw).
-template <int C, int NT, int X1 = 0, int PDM = DMX_TOK_PD>
+template <int C, int NT, int X1 = 0, int PDM = TOK_PD>
 DMX_DEV void tok_gemm_primed(const _Float16 (*Ah)[C + 8], const _Float16 (*Al)[C + 8], const TokW& w, int nw,
                              TokB<C, NT, PDM>& b, floatx16 (&acc)[NT], int arow0, int fr, int fh) {
   constexpr int S = C / 16, PD = TokB<C, NT, PDM>::PD;

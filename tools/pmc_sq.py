@@ -29,7 +29,7 @@ for d in sorted(glob.glob("gpurun_out/pmc_sq*")):
             acc[short(row["Kernel_Name"])][row["Counter_Name"]].append(float(row["Counter_Value"]))
 pat = sys.argv[1] if len(sys.argv) > 1 else "igemm|attention|norm"
 print(f"{'kernel':58s} {'n':>4s} {'cyc(k)':>8s} {'mfma%':>6s} {'lds%':>5s} {'w_any':>6s} {'w_inst':>6s} "
-      f"{'active':>6s} {'valu':>5s} {'ldsconf':>8s}")
+      f"{'active':>6s} {'valu':>5s} {'ldsconf':>8s} {'L2hit':>6s}")
 for k, c in sorted(acc.items()):
     if not re.search(pat, k):
         continue
@@ -42,4 +42,5 @@ for k, c in sorted(acc.items()):
     print(f"{k[:58]:58s} {n:4d} {kc / 1e3:8.1f} {100 * mf:6.1f} {100 * lds:5.1f} "
           f"{avg.get('SQ_WAIT_ANY', 0) / wc:6.2f} {avg.get('SQ_WAIT_INST_ANY', 0) / wc:6.2f} "
           f"{avg.get('SQ_ACTIVE_INST_ANY', 0) / wc:6.2f} {avg.get('SQ_ACTIVE_INST_VALU', 0) / wc:5.2f} "
-          f"{avg.get('SQ_LDS_BANK_CONFLICT', 0):8.3g}")
+          f"{avg.get('SQ_LDS_BANK_CONFLICT', 0):8.3g} "
+          f"{avg.get('TCC_HIT_sum', 0) / max(1.0, avg.get('TCC_HIT_sum', 0) + avg.get('TCC_MISS_sum', 0)):6.3f}")

@@ -1,4 +1,4 @@
-"""Winograd conv phase timing from a DMX_WSTAMP diagnostic build (MI355X only).
+"""Winograd conv phase timing from a DMX_DIAG diagnostic build (MI355X only).
 
   DMX_LIB=libwstamp.so python tools/wino_stamps.py [out.json]
 
@@ -45,7 +45,7 @@ def main():
     buf = (ctypes.c_ulonglong * (SLOTS * BLOCKS * 5))()
     n = lib.dmx_diag_wino_stamps(buf, len(buf))
     if n <= 0:
-        print("no stamps (not a DMX_WSTAMP build?)", n)
+        print("no stamps (not a DMX_DIAG build?)", n)
         return
     a = np.frombuffer(buf, dtype=np.uint64).reshape(SLOTS, BLOCKS, 5).astype(np.int64)
     out = []
