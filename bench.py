@@ -189,7 +189,7 @@ def legs(nm, model, x, y, vals, mask, args, tables, seed):
     assert torch.isfinite(x28).all(), "non-finite latents (28x28 leg)"
     out["latent28"] = {"value": round(k / dt, 3), "unit": "CFG batch-steps/s (B=%d, 28x28x4)" % args.batch,
                        "ms_per_step": round(dt / k * 1e3, 4), "steps": k,
-                       "pixel_rate_vs_32": None,  # filled in by main() (per-latent-pixel rate ratio)
+                       "pixel_rate_vs_main": None,  # filled in by main(): per-latent-pixel rate / the main leg's
                        "note": "reference default sampler shape (diff.py:315-322); the 28 / 14 / 7 / 3 maps run the "
                                "Winograd convs in their 32 / 16 / 8 / 4 geometries (zero-padded columns)"}
     return out
@@ -699,7 +699,9 @@ def main():
     if world == 1 and args.legs_steps > 0:
         out.update(legs(nm, model, x, y, vals, mask, args, tables, seed))
         if "latent28" in out:
-            out["latent28"]["pixel_rate_vs_32"] = round(out["latent28"]["value"] * 28 * 28 / (value * 32 * 32), 3)
+            # (the main leg runs at args.hw x args.hw: 32 x 32 by default)
+            out["latent28"]["pixel_rate_vs_main"] = round(out["latent28"]["value"] * 28 * 28 / (value * args.hw * args.hw), 3)
+            out["latent28"]["main_hw"] = args.hw
     if world == 1 and args.e2e:
         out["e2e"] = e2e_sample(model, args, dev)
     if args.sharded_T > 0:

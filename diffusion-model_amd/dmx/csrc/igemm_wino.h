@@ -154,6 +154,9 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   constexpr int CK = 16;                    // channels per chunk
   constexpr int NPC = RING0 ? SPB * W * W * (CK / 4) : HR * HC * (CK / 4);  // float4 pieces per chunk
   constexpr int NPI = (NPC + 511) / 512;    // pieces per thread
+  // W = 4: the zero rings written once before the loop are never a store_halo target — every piece
+  // is an interior pixel (NPC a whole number of 512-thread rounds, so no piece takes a scratch slot)
+  static_assert(!RING0 || NPC % 512 == 0, "W = 4: interior pieces must fill whole thread rounds");
   // epilogue LDS row pitch: 32 tiles + 2 — with 8-byte stores / reads, 34 cc mod 64 dwords puts
   // the 32 lanes of each ds_read_b64 group on 32 distinct bank pairs (a pitch of 36, needed by
   // 16-byte stores, made every read 2-way conflicted): Winograd launches -2 % in the eager
