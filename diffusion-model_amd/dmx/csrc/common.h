@@ -108,6 +108,15 @@ typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 // lo = f16(v - hi): v_fma_mix{lo,hi}_f16 computes v * 1.0 - hi with hi read as f16 and rounds
 // the exact result once to f16 — the same value as f16((float)(v - (float)hi)) (v - hi is
 // exact in fp32 by Sterbenz), in one VOP3P op per element instead of cvt + sub + cvt.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// 2^e with max|x| 2^e in [2^12, 2^13) from the bits of max|x| (0 / non-finite: e = 0)
+DMX_DEV int amax_exp(unsigned bits) {
+  const float mx = __uint_as_float(bits);
+  if (!(mx > 0.f) || !(mx < 3.0e38f)) return 0;
+  return min(100, max(-100, 12 - ilogbf(mx)));
+}
+
 DMX_DEV void split2u(float a, float b, unsigned& h, unsigned& l) {
   h = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){a, b}, half2v));
   unsigned t;

@@ -185,6 +185,8 @@ struct ConvW {
   _Float16* Uh = nullptr;       // 3x3 convs: Winograd F(2x2, 3x3) weights U = G g Gᵀ, split, fragment
   _Float16* Ul = nullptr;       // order (igemm_wino.h wino_pack_kernel), same 2^e scale as Bh / Bl
   float inv_scale = 1.f;
+  float* inv_dev = nullptr;     // device-side 2^-e of Bh / Bl (training data-gradient weights), or null
+  unsigned* amax_dev = nullptr; //   and the max|B| slot it comes from
   float* bias = nullptr;
   int cin = 0, cout = 0, taps = 0, kpad = 0, npad = 0, phases = 1;
 };
@@ -305,6 +307,7 @@ struct dmx_model {
   // tensors, in finalize order; the f16 planes of the split GEMMs are re-derived lazily
   // (planes_stale) before the next split-precision launch.
   std::vector<std::function<void(hipStream_t)>> jobs;
+  std::vector<std::function<void(hipStream_t)>> post_jobs;  // replayed after the repacks (device splits)
   std::vector<dmx::CopyJob> copies;     // parameter copies and weight repacks, replayed batched
   std::vector<dmx::RepackJob> repacks;  // (one launch each) by dmx_model_refresh
   void* job_tables = nullptr;           // device copies of the two tables
@@ -401,6 +404,38 @@ struct Packer {
   void job(std::function<void(hipStream_t)> f) {
     f(st);
     m->jobs.push_back(std::move(f));
+  }
+  // run now (after everything recorded so far) and on every refresh after the batched repacks
+  void post_job(std::function<void(hipStream_t)> f) {
+    f(st);
+    m->post_jobs.push_back(std::move(f));
+  }
+  // f16 hi / lo planes of a packed fp32 B with a device-side scale (no host round trip), re-derived
+  // on the device after every refresh: the training data-gradient weights (train_engine.h)
+  void split_dev(ConvW& c) {
+    const size_t n = (size_t)c.phases * c.npad * c.kpad;
+    void* h = nullptr;
+    void* l = nullptr;
+    void* a = nullptr;
+    HIPCHK(hipMalloc(&h, n * sizeof(_Float16)));
+    m->owned.push_back(h);
+    HIPCHK(hipMalloc(&l, n * sizeof(_Float16)));
+    m->owned.push_back(l);
+    constexpr int NP = 64;  // partial maxima of the weight's absmax
+    HIPCHK(hipMalloc(&a, NP * sizeof(unsigned) + 64));
+    m->owned.push_back(a);
+    c.Bh = static_cast<_Float16*>(h);
+    c.Bl = static_cast<_Float16*>(l);
+    c.amax_dev = static_cast<unsigned*>(a);
+    c.inv_dev = reinterpret_cast<float*>(static_cast<char*>(a) + NP * sizeof(unsigned));
+    const ConvW cc = c;
+    post_job([cc, n](hipStream_t s) {
+      absmax_part_kernel<<<NP, 256, 0, s>>>(cc.B, n, cc.amax_dev);
+      HIPCHK(hipGetLastError());
+      split_weights_dev_kernel<<<(int)std::min<size_t>((n + 255) / 256, 8192), 256, 0, s>>>(cc.B, cc.Bh, cc.Bl, n,
+                                                                                            cc.amax_dev, NP, cc.inv_dev);
+      HIPCHK(hipGetLastError());
+    });
   }
   float* copy(const std::string& name) {
     auto& t = in(name);
@@ -755,6 +790,15 @@ struct Run {
   // decoded bytes do not depend on the batch or chunk it is decoded in (summation order is a
   // function of the per-sample geometry only).
   int tile_n = 0;
+  // non-null: the next gemm() runs the split-precision implicit GEMM with A scaled on the device by
+  // this max|A| slot (training data gradients, train_engine.h dgrad)
+  const unsigned* a_amax = nullptr;
+  int a_nparts = 0;  // a_amax: that many per-block partial maxima (absmax_part_kernel)
+  // train_engine.h dy_amax: the last tensor whose |max| partials were taken
+  const float* amax_src = nullptr;
+  size_t amax_n = 0;
+  unsigned* amax_slot = nullptr;
+  int amax_parts = 0;
   void tap(const std::string& name, const float* p, size_t count);
   std::string ck_layer;
   // DMX_CKSUM: one workspace checksum per layer, taken when the next layer's first kernel begins
@@ -1063,7 +1107,11 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   const int tiles128 = cdiv(Md, 128) * cdiv(cw.cout, bn) * cw.phases;
   const int bm = tiles128 >= 256 ? 128 : 64;  // 128-row tiles (split K if the grid is then small) from 256 tiles
   const int blocks = cdiv(Md, bm) * cdiv(cw.cout, bn) * cw.phases;
-  const bool x3 = R.m->prec >= 1 && src_mode == SRC_PLAIN && cw.Bh != nullptr;
+  // (R.a_amax: a training data gradient on the split GEMM with device-side operand scales — whatever
+  // the model's precision mode, only the implicit-GEMM kernels below carry those scales)
+  const bool x3 = (R.m->prec >= 1 || R.a_amax != nullptr) && src_mode == SRC_PLAIN && cw.Bh != nullptr;
+  if (R.a_amax != nullptr && (!x3 || ash != nullptr || epi == EPI_STATS || gn != nullptr || R.m->prec == 2))
+    throw Error(DMX_E_INTERNAL, "gemm: device-scaled operands only on the plain split implicit GEMM");
   const bool x1 = x3 && R.m->prec == 2;  // config-4 fp16: one MFMA on the hi planes
   // 512-thread ping-pong kernel (256-row tiles) for the large f16-plane convs
   const bool pp = pp_enabled() && x3 && epi == EPI_STATS && cw.phases == 1 && s.C >= 32 && ash != nullptr &&
@@ -1166,6 +1214,9 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   xp.gn_res = nullptr;
   xp.Uh = xp.Ul = nullptr;
   xp.u_bytes = 0;
+  xp.a_amax = R.a_amax;
+  xp.a_nparts = R.a_nparts;
+  xp.w_inv = cw.inv_dev;
   {
     const size_t a_el = (size_t)N * p.Hin * p.Win * s.C;
     const size_t ab = a_el * (ash != nullptr ? 2 : 4), bb = (size_t)cw.npad * cw.kpad * 2;

@@ -47,10 +47,18 @@ struct X3Params {
   const _Float16* Ul;
   unsigned u_bytes;          // bytes of one U plane (16 * Cout * Cin f16)
   int dslot;                 // diagnostic builds (DMX_DIAG): stamp slot of this launch, else unused
+  // Device-side operand scales (igemm_x3_kernel, fp32 A source; the training data gradients, whose dY
+  // and refreshed weights have no host-known range): a_amax = bits of max|A| — A is multiplied by
+  // 2^ea (max|A| 2^ea in [2^12, 2^13)) before its hi / lo split, so the lo parts stay f16-normal;
+  // w_inv = the weights' 2^-e written by split_weights_dev_kernel.  The accumulators are multiplied
+  // by w_inv 2^-ea (exact: powers of two).  Null: host inv_scale, unscaled A.
+  const unsigned* a_amax;     // (a_nparts > 0: a_amax holds that many per-block partial maxima)
+  int a_nparts;
+  const float* w_inv;
 };
 
 
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
 
 // Buffer-resource loads (32-bit offsets, descriptor in SGPRs): an offset at or past the range
 // returns zeros, which is how padding taps / rows past M are masked.
@@ -135,6 +143,18 @@ __global__ __launch_bounds__(64 * NW) void igemm_x3_kernel(const X3Params P) {
     lc = k - ltap * C;
   };
   const float* __restrict__ asrc = p.src.src0;
+  float a_sc = 1.f, o_sc = P.inv_scale;  // device-side scales (X3Params::a_amax / w_inv)
+  const bool ascale = !SPLIT_A && P.a_amax != nullptr;
+  if (P.w_inv != nullptr) o_sc = *P.w_inv;
+  if (!SPLIT_A && P.a_amax != nullptr) {
+    unsigned mb = P.a_nparts > 0 ? 0u : *P.a_amax;
+    for (int i = lane; i < P.a_nparts; i += 64) mb = max(mb, P.a_amax[i]);  // (non-negative floats order as uints)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mb = max(mb, (unsigned)__shfl_xor((int)mb, o, 64));
+    const int ea = amax_exp(mb);
+    a_sc = ldexpf(1.f, ea);
+    o_sc = o_sc * ldexpf(1.f, -ea);
+  }
   // Buffer-resource addressing: 32-bit byte offsets; a masked piece gets an out-of-range offset
   // and reads zeros (no 64-bit address math / selects per piece); B offsets are per-thread
   // constants plus a wave-uniform K-tile offset.
@@ -186,7 +206,12 @@ __global__ __launch_bounds__(64 * NW) void igemm_x3_kernel(const X3Params P) {
         *reinterpret_cast<half4*>(&Ah[buf][ra + i * ARS][qa * 4]) = __builtin_convertvector(ra4[st][i], half4);
       } else {
         half4 h, l;
-        split4(ra4[st][i], h, l);
+        floatx4 v = ra4[st][i];
+        if (ascale) {  // (uniform: training data gradients only)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] *= a_sc;
+        }
+        split4(v, h, l);
         *reinterpret_cast<half4*>(&Ah[buf][ra + i * ARS][qa * 4]) = h;
         *reinterpret_cast<half4*>(&Al[buf][ra + i * ARS][qa * 4]) = l;
       }
@@ -301,13 +326,48 @@ __global__ __launch_bounds__(64 * NW) void igemm_x3_kernel(const X3Params P) {
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] *= P.inv_scale;
+      for (int r = 0; r < 16; ++r) acc[i][j][r] *= o_sc;
 
   // the shared epilogue's 2 x 2 wave grid: column pairs of waves as separate BN / (NW / 2) halves
   igemm_epilogue<BM, 2 * WN, EPI>(p, acc, phase, m0, n0 + (wn >> 1) * 2 * WN, wm, wn & 1, fr, fh);
 }
 
 static __global__ void split_weights_kernel(const float* src, _Float16* hi, _Float16* lo, size_t n, float scale) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const float v = src[i] * scale;
+    const _Float16 h = (_Float16)v;
+    hi[i] = h;
+    lo[i] = (_Float16)(v - (float)h);
+  }
+}
+
+// Per-block partial maxima (no atomics, no zeroed slot): part[blockIdx.x] = bits of max|src| over
+// the block's grid-stride share; consumers reduce the gridDim.x partials (X3Params::a_nparts).
+static __global__ __launch_bounds__(256) void absmax_part_kernel(const float* src, size_t n, unsigned* part) {
+  float m = 0.f;
+  const size_t n4 = n / 4;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+    const floatx4 v = reinterpret_cast<const floatx4*>(src)[i];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+  }
+  for (size_t i = n4 * 4 + (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    m = fmaxf(m, fabsf(src[i]));
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  __shared__ float wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3])));
+}
+
+// Split with a device-side scale: max|w| 2^e in [2^12, 2^13) from *amax (absmax_kernel), 2^-e to *inv
+// (the training data-gradient weights, re-split on the device after every parameter refresh).
+static __global__ void split_weights_dev_kernel(const float* src, _Float16* hi, _Float16* lo, size_t n,
+                                                const unsigned* amax, int nparts, float* inv) {
+  unsigned mb = 0u;  // (absmax_part_kernel's per-block maxima)
+  for (int i = 0; i < nparts; ++i) mb = max(mb, amax[i]);
+  const int e = amax_exp(mb);
+  const float scale = ldexpf(1.f, e);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *inv = ldexpf(1.f, -e);
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     const float v = src[i] * scale;
     const _Float16 h = (_Float16)v;

@@ -321,7 +321,12 @@ struct WgradParams {
   int M, K;          // M = N*H*W rows, K = taps * Cin
   int rows_per_split;
   float* part;       // [splits][Cout][K]
-  float* bpart;      // wgrad_fast_kernel: [splits][Cout] column sums of dY (bias gradient), or null
+  float* bpart;      // wgrad_x3_kernel: [splits][Cout] column sums of dY (bias gradient), or null
+  // wgrad_x3_kernel (the f16 matrix cores, x3 split, fp32 accumulate): dY scaled on the device by 2^ea
+  // from its max (dy_nparts per-block partial maxima, absmax_part_kernel); X (tape activations, O(1))
+  // split as is
+  const unsigned* dy_amax;
+  int dy_nparts;
 };
 
 static __global__ __launch_bounds__(256) void wgrad_kernel(const WgradParams p) {
@@ -372,29 +377,50 @@ static __global__ __launch_bounds__(256) void wgrad_kernel(const WgradParams p) 
   }
 }
 
-// Fast path (Cin % 64 == 0, Cout % 64 == 0): block tile 64 (co) x 128 (k), the rows streamed in
-// stages of 32 through double-buffered LDS with float4 global loads issued one stage ahead
-// (register prefetch), 4 waves 2 x 2 each owning 32 co x 64 k (two 32x32 accumulators).
-// A 64-wide k slice lies inside one tap (Cin % 64 == 0), so a thread's tap / channel offset is
-// fixed and only its rows' (n, y, x) are decoded per stage.
-constexpr int WG_BM = 32;
-static __global__ __launch_bounds__(256) void wgrad_fast_kernel(const WgradParams p) {
-  __shared__ __attribute__((aligned(16))) float dys[2][WG_BM][64 + 4];
-  __shared__ __attribute__((aligned(16))) float xs[2][WG_BM][128 + 4];
+// Weight gradient on the f16 matrix cores (x3 split, fp32 accumulate): the tiling of round 5's fp32
+// kernel (64 Cout x 128 K per block, 2 x 2 waves of 32 x 64, 32-row stages, double-buffered), with the staged
+// rows split once into f16 hi / lo planes kept row-major in LDS ([m][co], [m][k]) and the MFMA operands
+// — contraction over m, 8 consecutive rows per lane — read with ds_read_b64_tr_b16: per 16-lane group a
+// 4-row x 16-column block, lane 4q + p addressing row q, columns 4p .. 4p + 3, lane i receiving column i
+// (MI355X guide T10).  dY is multiplied by 2^ea (its max |dY| 2^ea in [2^12, 2^13): the lo parts stay
+// f16-normal) and the slabs by 2^-ea.  Row pitches of 96 / 160 halves (48 / 80 banks: the 4 rows of a
+// block on 4 disjoint 16-bank ranges) make the transposed reads conflict-free.  The bias gradient
+// (column sums of dY) is summed from the staged registers: lanes, then the 4 waves in a fixed order.
+constexpr int WG_BM = 32;  // rows per stage
+typedef __fp16 fp16x4_t __attribute__((__vector_size__(4 * sizeof(__fp16))));
+DMX_DEV half4 lds_tr16(const _Float16* p) {
+  return __builtin_bit_cast(half4, __builtin_amdgcn_ds_read_tr16_b64_v4f16(
+                                       (__attribute__((address_space(3))) fp16x4_t*)(p)));
+}
+static __global__ __launch_bounds__(256) void wgrad_x3_kernel(const WgradParams p) {
+  constexpr int DP = 96, XP = 160;  // plane row pitches (halves)
+  __shared__ __attribute__((aligned(16))) _Float16 Dh[2][WG_BM][DP];
+  __shared__ __attribute__((aligned(16))) _Float16 Dl[2][WG_BM][DP];
+  __shared__ __attribute__((aligned(16))) _Float16 Xh[2][WG_BM][XP];
+  __shared__ __attribute__((aligned(16))) _Float16 Xl[2][WG_BM][XP];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv >> 1, wn = wv & 1;
   const int co0 = blockIdx.x * 64, k0 = blockIdx.y * 128;
   const int mbeg = blockIdx.z * p.rows_per_split, mend = min(p.M, mbeg + p.rows_per_split);
   const int HW = p.H * p.W;
-  // dY: 32 rows x 16 float4 -> thread (row tid / 16 + 16 i, float4 tid % 16), i < 2
-  const int dr = tid >> 4, dc = (tid & 15) * 4;
-  // X: 32 rows x 32 float4 -> thread (row tid / 32 + 8 i, float4 tid % 32), i < 4
-  const int xr = tid >> 5, xc = (tid & 31) * 4;
+  const float rhw = 1.f / (float)HW, rw = 1.f / (float)p.W;
+  const int dr = tid >> 4, dc = (tid & 15) * 4;  // dY: rows dr + 16 i (i < 2), float4 dc
+  const int xr = tid >> 5, xc = (tid & 31) * 4;  // X: rows xr + 8 i (i < 4), float4 xc
   const int k = k0 + xc;
   const bool kvalid = k < p.K;
   const int tap = kvalid ? k / p.Cin : 0, ci = k - tap * p.Cin;
   const int ty = p.taps == 9 ? tap / 3 - 1 : 0, tx = p.taps == 9 ? tap % 3 - 1 : 0;
-  floatx4 rd[2], rx[4];
-  auto load = [&](int m0) {
+  unsigned mb = 0u;
+  for (int i = lane; i < p.dy_nparts; i += 64) mb = max(mb, p.dy_amax[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mb = max(mb, (unsigned)__shfl_xor((int)mb, o, 64));
+  const int ea = amax_exp(mb);
+  const float a_sc = ldexpf(1.f, ea), o_sc = ldexpf(1.f, -ea);
+  const bool bias = p.bpart != nullptr && blockIdx.y == 0;
+  floatx4 bs = {0.f, 0.f, 0.f, 0.f};  // column sums of dY (columns dc .. dc + 3) over this thread's rows
+  floatx4 rdv[2][2], rxv[2][4];  // two register stages (the loads run two 32-row stages ahead)
+  auto load = [&](int m0, int rs) {
+    floatx4(&rd)[2] = rdv[rs];
+    floatx4(&rx)[4] = rxv[rs];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int m = m0 + dr + 16 * i;
@@ -406,7 +432,12 @@ static __global__ __launch_bounds__(256) void wgrad_fast_kernel(const WgradParam
       const int m = m0 + xr + 8 * i;
       floatx4 v = {0.f, 0.f, 0.f, 0.f};
       if (m < mend && kvalid) {
-        const int n = m / HW, rr = m - n * HW, y = rr / p.W, xx = rr - y * p.W;
+        // (division by HW and W through the float reciprocal plus one correction step: exact for the
+        // M < 2^24 rows here)
+        int n = (int)((float)m * rhw), rr = m - n * HW;
+        if (rr < 0) { --n; rr += HW; } else if (rr >= HW) { ++n; rr -= HW; }
+        int y = (int)((float)rr * rw), xx = rr - y * p.W;
+        if (xx < 0) { --y; xx += p.W; } else if (xx >= p.W) { ++y; xx -= p.W; }
         const int iy = y + ty, ix = xx + tx;
         if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W)
           v = *reinterpret_cast<const floatx4*>(p.x + (((size_t)n * p.H + iy) * p.W + ix) * p.Cin + ci);
@@ -414,44 +445,86 @@ static __global__ __launch_bounds__(256) void wgrad_fast_kernel(const WgradParam
       rx[i] = v;
     }
   };
-  auto store = [&](int b) {
+  auto store = [&](int b, int rs) {
+    floatx4(&rd)[2] = rdv[rs];
+    floatx4(&rx)[4] = rxv[rs];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) *reinterpret_cast<floatx4*>(&dys[b][dr + 16 * i][dc]) = rd[i];
+    for (int i = 0; i < 2; ++i) {
+      if (bias) bs += rd[i];
+      floatx4 v = rd[i];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<floatx4*>(&xs[b][xr + 8 * i][xc]) = rx[i];
+      for (int e = 0; e < 4; ++e) v[e] *= a_sc;
+      half4 h, l;
+      split4(v, h, l);
+      *reinterpret_cast<half4*>(&Dh[b][dr + 16 * i][dc]) = h;
+      *reinterpret_cast<half4*>(&Dl[b][dr + 16 * i][dc]) = l;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      half4 h, l;
+      split4(rx[i], h, l);
+      *reinterpret_cast<half4*>(&Xh[b][xr + 8 * i][xc]) = h;
+      *reinterpret_cast<half4*>(&Xl[b][xr + 8 * i][xc]) = l;
+    }
   };
   floatx16 acc[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
-  const bool bias = p.bpart != nullptr && blockIdx.y == 0;
-  float bsum = 0.f;  // threads 0..63 of a k-tile-0 block: column sum of dY over this split's rows
+  // transposed-read addressing: group g = lane / 16 (rows + 8 for g >= 2, columns + 16 for odd g),
+  // lane 4q + p of the group -> row q, columns 4p .. 4p + 3
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int trow = 8 * (g >> 1) + q, tcol = 16 * (g & 1) + 4 * pp;
   const int nst = (mend - mbeg + WG_BM - 1) / WG_BM;
-  if (nst > 0) {
-    load(mbeg);
-    store(0);
-  }
-  __syncthreads();
-  for (int st = 0; st < nst; ++st) {
-    const int b = st & 1;
-    if (st + 1 < nst) load(mbeg + (st + 1) * WG_BM);
+  auto compute = [&](int b) {
 #pragma unroll
-    for (int s = 0; s < WG_BM; s += 2) {
-      const float a = dys[b][s + (lane >> 5)][wm * 32 + (lane & 31)];
-      const float b0 = xs[b][s + (lane >> 5)][wn * 64 + (lane & 31)];
-      const float b1 = xs[b][s + (lane >> 5)][wn * 64 + 32 + (lane & 31)];
-      acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b0, acc[0], 0, 0, 0);
-      acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b1, acc[1], 0, 0, 0);
+    for (int s = 0; s < WG_BM; s += 16) {
+      const int r0 = s + trow;
+      const half4 a0 = lds_tr16(&Dh[b][r0][wm * 32 + tcol]), a1 = lds_tr16(&Dh[b][r0 + 4][wm * 32 + tcol]);
+      const half4 c0 = lds_tr16(&Dl[b][r0][wm * 32 + tcol]), c1 = lds_tr16(&Dl[b][r0 + 4][wm * 32 + tcol]);
+      const half8 ah = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+      const half8 al = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+#pragma unroll
+      for (int n = 0; n < 2; ++n) {
+        const int cx = wn * 64 + 32 * n + tcol;
+        const half4 b0 = lds_tr16(&Xh[b][r0][cx]), b1 = lds_tr16(&Xh[b][r0 + 4][cx]);
+        const half4 d0 = lds_tr16(&Xl[b][r0][cx]), d1 = lds_tr16(&Xl[b][r0 + 4][cx]);
+        const half8 bh = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+        const half8 bl = {d0[0], d0[1], d0[2], d0[3], d1[0], d1[1], d1[2], d1[3]};
+        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[n], 0, 0, 0);
+        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[n], 0, 0, 0);
+        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[n], 0, 0, 0);
+      }
     }
-    if (bias && tid < 64) {
-#pragma unroll 8
-      for (int s = 0; s < WG_BM; ++s) bsum += dys[b][s][tid];
-    }
-    if (st + 1 < nst) store(b ^ 1);
+  };
+  // stage st lives in register set st & 1 and LDS buffer st & 1; its loads are issued two stages
+  // ahead (before stage st - 2's MFMAs), its store after stage st - 1's MFMAs
+  if (nst > 0) load(mbeg, 0);
+  if (nst > 1) load(mbeg + WG_BM, 1);
+  if (nst > 0) store(0, 0);
+  __syncthreads();
+  auto body = [&](int st, int rs) {  // rs = st & 1 (compile-time at both call sites)
+    if (st + 2 < nst) load(mbeg + (st + 2) * WG_BM, rs);  // (set rs was stored one iteration ago)
+    compute(rs);
+    if (st + 1 < nst) store(rs ^ 1, rs ^ 1);
     __syncthreads();
+  };
+  for (int st = 0; st < nst; st += 2) {
+    body(st, 0);
+    if (st + 1 < nst) body(st + 1, 1);
   }
-  if (bias && tid < 64) p.bpart[(size_t)blockIdx.z * p.Cout + co0 + tid] = bsum;
+  if (bias) {  // lanes sharing columns (xor 16, 32), then waves 0..3 in order through LDS
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      bs[e] += __shfl_xor(bs[e], 16, 64);
+      bs[e] += __shfl_xor(bs[e], 32, 64);
+    }
+    float* red = reinterpret_cast<float*>(&Dh[0][0][0]);  // (the stages are done: last barrier above)
+    if (lane < 16) *reinterpret_cast<floatx4*>(&red[wv * 64 + dc]) = bs;
+    __syncthreads();
+    if (tid < 64) p.bpart[(size_t)blockIdx.z * p.Cout + co0 + tid] = ((red[tid] + red[64 + tid]) + red[128 + tid]) + red[192 + tid];
+  }
   float* dst = p.part + (size_t)blockIdx.z * p.Cout * p.K;
 #pragma unroll
   for (int j = 0; j < 2; ++j)
@@ -459,7 +532,7 @@ static __global__ __launch_bounds__(256) void wgrad_fast_kernel(const WgradParam
     for (int r = 0; r < 16; ++r) {
       const int co = co0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
       const int kk = k0 + wn * 64 + j * 32 + (lane & 31);
-      if (kk < p.K) dst[(size_t)co * p.K + kk] = acc[j][r];
+      if (kk < p.K) dst[(size_t)co * p.K + kk] = acc[j][r] * o_sc;
     }
 }
 

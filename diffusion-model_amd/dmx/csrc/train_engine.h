@@ -152,6 +152,7 @@ static ConvW pack_dgrad_conv(Packer& P, const std::string& wname, int cin, int c
     HIPCHK(hipGetLastError());
   });
   P.repack(c.B, tmp, 0, 1, c.npad, c.kpad, cin, cout, 3);
+  P.split_dev(c);
   return c;
 }
 
@@ -166,6 +167,7 @@ static ConvW pack_dgrad_linear(Packer& P, const std::string& wname, int fin, int
   c.B = P.alloc((size_t)c.npad * c.kpad);
   float* tmp = P.transposed(wname, fout, fin);
   P.repack(c.B, tmp, 1, 1, c.npad, c.kpad, fin, fout, 1);
+  P.split_dev(c);
   return c;
 }
 
@@ -497,24 +499,55 @@ static void colsum_pair(Run& R, const float* in, int rows, int C, size_t stride,
 // bias gradient = column sums of dY [M][C]
 static void bias_grad(Run& R, const float* dy, int M, int C, float* out) { colsum(R, dy, M, C, C, out); }
 
+// Per-block partial maxima of |dY| for the device-side operand scale of the f16-core data and weight
+// gradients (X3Params::a_amax, WgradParams::dy_amax).  The weight and data gradients of a layer read
+// the same dY back to back (wgrad, then dgrad): the measurement is reused once, by the very next call
+// on the same tensor, and then dropped — a later call on that buffer (its content may have changed)
+// measures again.  Same decisions in the plan and the real pass (arena pointers correspond one to one).
+static const unsigned* dy_amax(Run& R, const float* dy, size_t n, int* parts) {
+  if (R.amax_src == dy && R.amax_n == n) {
+    R.amax_src = nullptr;  // (single use)
+    *parts = R.amax_parts;
+    return R.amax_slot;
+  }
+  const int np = (int)std::min<size_t>((n + 4095) / 4096, 256);  // (>= 4 float4 per thread)
+  unsigned* slot = R.ws.get<unsigned>(256);
+  if (!R.plan) {
+    R.begin("absmax_part_kernel", 0.0, 4.0 * (double)n);
+    absmax_part_kernel<<<np, 256, 0, R.st>>>(dy, n, slot);
+    R.end();
+    HIPCHK(hipGetLastError());
+  }
+  R.amax_src = dy;
+  R.amax_n = n;
+  R.amax_slot = slot;
+  R.amax_parts = np;
+  *parts = np;
+  return slot;
+}
+
 // weight gradient of a conv3x3 (taps 9) / Linear (taps 1) over NHWC input x and NHWC dY
 static void wgrad(Run& R, const float* dy, const float* x, int N, int H, int W, int Cin, int Cout, int taps,
                   int cin_real, float* grad, float* bias_grad_out = nullptr) {
   const int M = N * H * W, K = taps * Cin;
   const bool fast = Cin % 64 == 0 && Cout % 64 == 0;
   const int bxy = cdiv(Cout, 64) * cdiv(K, fast ? 128 : 64);
-  int splits = std::max(1, std::min(cdiv(1024, bxy), cdiv(M, 256)));
+  // (the x3 kernel runs two 64 KB-LDS blocks per CU: one round of 512 blocks; fewer slabs for
+  // wgrad_finish_kernel to read than the fp32 kernel's 1024-block target)
+  int splits = std::max(1, std::min(cdiv(fast ? 512 : 1024, bxy), cdiv(M, 256)));
   const int rps = rup(cdiv(M, splits), 16);
   splits = cdiv(M, rps);
   float* part = R.ws.get<float>((size_t)splits * Cout * K);
   // bias gradient: column sums of dY, from the fast kernel's k-tile-0 blocks (per split)
   float* bpart = (bias_grad_out != nullptr && fast) ? R.ws.get<float>((size_t)splits * Cout) : nullptr;
+  int nparts = 0;
+  const unsigned* amax = fast ? dy_amax(R, dy, (size_t)M * Cout, &nparts) : nullptr;  // (x3 products)
   if (!R.plan) {
     check_range(R, dy, (size_t)M * Cout * 4, "wgrad dY");
     check_range(R, x, (size_t)M * Cin * 4, "wgrad X");
-    WgradParams p{dy, x, N, H, W, Cin, Cout, taps, M, K, rps, part, bpart};
+    WgradParams p{dy, x, N, H, W, Cin, Cout, taps, M, K, rps, part, bpart, amax, nparts};
     R.begin("wgrad_kernel", 2.0 * M * (double)Cout * K, 4.0 * ((double)M * (Cout + Cin) + (double)splits * Cout * K));
-    if (fast) wgrad_fast_kernel<<<dim3(Cout / 64, cdiv(K, 128), splits), 256, 0, R.st>>>(p);
+    if (fast) wgrad_x3_kernel<<<dim3(Cout / 64, cdiv(K, 128), splits), 256, 0, R.st>>>(p);
     else wgrad_kernel<<<dim3(cdiv(Cout, 64), cdiv(K, 64), splits), 256, 0, R.st>>>(p);
     R.end();
     HIPCHK(hipGetLastError());
@@ -529,9 +562,25 @@ static void wgrad(Run& R, const float* dy, const float* x, int N, int H, int W, 
 }
 
 // data gradient through a packed transposed / flipped weight: dx (+)= dY * W'
+// On the f16 matrix cores (x3 split, fp32 accumulate): dY is scaled by a power of two from its own
+// max|dY| before the split (gradients sit far below f16's normal range; unscaled, their lo parts went
+// subnormal — 4.6e-4 rel-L2, round 2) and the weights carry a device-side scale refreshed with them
+// (Packer::split_dev), so nothing waits on the host.
 static void dgrad(Run& R, const float* dy, int Cy, int N, int H, int W, const ConvW& dw, float* dx, bool accumulate) {
-  gemm(R, plain_src(dy, Cy), SRC_PLAIN, N, H, W, dw, accumulate ? EPI_BIAS_RES : EPI_BIAS, dx,
-       accumulate ? dx : nullptr, nullptr, 1);
+  int parts = 0;
+  const unsigned* amax = dy_amax(R, dy, (size_t)N * H * W * Cy, &parts);
+  R.a_amax = amax;
+  R.a_nparts = parts;
+  try {
+    gemm(R, plain_src(dy, Cy), SRC_PLAIN, N, H, W, dw, accumulate ? EPI_BIAS_RES : EPI_BIAS, dx,
+         accumulate ? dx : nullptr, nullptr, 1);
+  } catch (...) {
+    R.a_amax = nullptr;
+    R.a_nparts = 0;
+    throw;
+  }
+  R.a_amax = nullptr;
+  R.a_nparts = 0;
 }
 
 static void gn_bwd_launch(Run& R, const float* r, const float2* rp, int nseg, int rrows, const Vec& g, const Vec& b,
@@ -881,6 +930,7 @@ static void refresh_model(dmx_model* m, hipStream_t st) {
     repack_batch_kernel<<<dim3(64, (unsigned)nr), 256, 0, st>>>(rt);
     HIPCHK(hipGetLastError());
   }
+  for (auto& f : m->post_jobs) f(st);  // device-side splits of the data-gradient weights
   m->planes_stale = true;
 }
 
