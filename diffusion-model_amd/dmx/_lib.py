@@ -105,6 +105,7 @@ SIGNATURES = [
     ("dmx_debug_num_taps", _I, [_P]),
     ("dmx_debug_tap", _I, [_P, _I, ctypes.c_char_p, _I, ctypes.POINTER(_I64), _P, _P]),
     ("dmx_step_profile", _I, [_P, ctypes.POINTER(StepArgs), ctypes.POINTER(KernelRecord), _I, ctypes.POINTER(_I), _P]),
+    ("dmx_attn_core_backward", _I, [_P, _P, _P, _P, _I, _I, _I, _P]),
     ("dmx_diag_wino_stamps", _I, [_P, _I]),
 ]
 
@@ -126,6 +127,8 @@ def load():
         except OSError as e:  # pragma: no cover - environment specific
             raise DmxUnavailable(f"cannot load {LIB_PATH}: {e}") from e
         for name, res, args in SIGNATURES:
+            if "DMX_LIB" in os.environ and not hasattr(lib, name):
+                continue  # an older A/B build may predate a symbol
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args

@@ -1535,10 +1535,13 @@ static void layernorm(Run& R, const float* x, float* y, const Vec& w, const Vec&
   HIPCHK(hipGetLastError());
 }
 
-static void attention_core(Run& R, const float* qkv, float* out, int N, int L, int C) {
+// stats (training forward only, exact fp32): the row max / 1 / sum per (sample, head, query) for
+// the backward (train_engine.h attn_core_bwd)
+static void attention_core(Run& R, const float* qkv, float* out, int N, int L, int C, float* stats = nullptr) {
   if (R.plan) return;
   const int D = C / 4;
   if (D != 16 && D != 32 && D != 64) throw Error(DMX_E_INTERNAL, "attention: unsupported head dim");
+  if (stats != nullptr && R.m->prec != 0) throw Error(DMX_E_INTERNAL, "attention stats: exact-fp32 mode only");
   if (R.m->prec >= 1 && D == 16 && att16_lds_bytes(L, 0) <= 160 * 1024) {
     // head resident in LDS (sa5 / sa6): one block per (sample, head), no per-chunk staging
     const int x1 = R.m->prec == 2 ? 1 : 0, nw = L > 256 ? 16 : 8;
@@ -1563,7 +1566,7 @@ static void attention_core(Run& R, const float* qkv, float* out, int N, int L, i
   dim3 grid(cdiv(L, 64 * qt), 4, N);
   R.begin("attention_kernel<" + std::to_string(D) + ", " + std::to_string(qt) + ">", 4.0 * N * (double)L * L * C,
           4.0 * (double)N * L * 4 * C);
-  launch_attention_f32(D, qt, qkv, out, L, C, grid, R.st);
+  launch_attention_f32(D, qt, qkv, out, L, C, grid, R.st, stats);
   R.end();
   HIPCHK(hipGetLastError());
 }
@@ -2331,6 +2334,19 @@ int dmx_train_backward(dmx_model* m, int64_t tape_id, const float* d_eps, const 
     with_fp32(m, [&] {
       run_arena(m, st, m->bws, m->bws_mem, m->bws_cap, [&](Run& R) { train_bwd_body(R, *m->tape, G, d_eps, d_geom); });
     });
+  });
+}
+
+int dmx_attn_core_backward(const float* qkv, const float* o, const float* dout, float* dqkv, int n, int L, int C,
+                           void* stream) {
+  return guarded([&] {
+    REQUIRE(qkv && o && dout && dqkv, "null tensor");
+    REQUIRE(n >= 1 && L >= 1 && (C == 64 || C == 128 || C == 256), "attention backward: n, L >= 1, C in {64, 128, 256}");
+    hipStream_t st = (hipStream_t)stream;
+    float* sbuf = nullptr;
+    HIPCHK(hipMallocAsync(reinterpret_cast<void**>(&sbuf), (size_t)n * 4 * L * 3 * sizeof(float), st));
+    attn_core_bwd_launch(qkv, o, dout, dqkv, sbuf, n, L, C, false, st);
+    HIPCHK(hipFreeAsync(sbuf, st));
   });
 }
 

@@ -34,8 +34,9 @@ void launch_f32(int src_mode, int epi, int bm, int bn, const IgemmParams& p, dim
   }
 }
 
-void launch_attention_f32(int D, int qt, const float* qkv, float* out, int L, int C, dim3 grid, hipStream_t st) {
-#define ATT(DD, QQ) attention_kernel<DD, QQ><<<grid, 256, 0, st>>>(qkv, out, L, C)
+void launch_attention_f32(int D, int qt, const float* qkv, float* out, int L, int C, dim3 grid, hipStream_t st,
+                          float* stats) {
+#define ATT(DD, QQ) attention_kernel<DD, QQ><<<grid, 256, 0, st>>>(qkv, out, L, C, stats)
   if (D == 16) { if (qt == 2) ATT(16, 2); else ATT(16, 1); }
   else if (D == 32) { if (qt == 2) ATT(32, 2); else ATT(32, 1); }
   else { if (qt == 2) ATT(64, 2); else ATT(64, 1); }

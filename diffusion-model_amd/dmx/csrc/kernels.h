@@ -573,10 +573,12 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* x, float* y
 // softmax(q k^T / sqrt(D)) v per (sample, head)  (nn.MultiheadAttention, 4 heads,
 // models/unet_cond.py:36,49).  Computed transposed (S^T = K Q^T, O^T = V^T P^T) so
 // the query sits on the lane: the P accumulator is directly the B operand of PV.
-// Each wave owns 16*QT queries; 64-key K/V chunks are staged in LDS.
+// Each wave owns 16*QT queries; 64-key K/V chunks are staged in LDS.  st (training forward, else
+// null): per (sample, head, query) the row max m and 1 / sum l, [N][4][L][3] (slot 2 is the
+// backward's, train.h attn_dq_mfma_kernel).
 // ---------------------------------------------------------------------------
 template <int D, int QT>
-__global__ __launch_bounds__(256) void attention_kernel(const float* qkv, float* out, int L, int C) {
+__global__ __launch_bounds__(256) void attention_kernel(const float* qkv, float* out, int L, int C, float* st) {
   constexpr int KC = 64, DS = D + 4, DP = D / 4;
   __shared__ __attribute__((aligned(16))) float Ks[KC][DS];
   __shared__ __attribute__((aligned(16))) float Vs[KC][DS];
@@ -688,6 +690,11 @@ __global__ __launch_bounds__(256) void attention_kernel(const float* qkv, float*
     l += __shfl_xor(l, 32, 64);
     const float inv = 1.0f / l;
     const int qi = blockIdx.x * (64 * QT) + wid * 16 * QT + qt * 16 + ql;
+    if (st != nullptr && g == 0 && qi < L) {
+      float* so = st + (((size_t)n * 4 + hd) * L + qi) * 3;
+      so[0] = mrun[qt];
+      so[1] = inv;
+    }
     if (qi < L) {
 #pragma unroll
       for (int dt = 0; dt < D / 16; ++dt) {

@@ -48,7 +48,8 @@ void launch_attention_x3(int D, int wpe, int x1, const float* qkv, float* out, i
                          hipStream_t st);
 // D = 16 core with the head resident in LDS; grid (1, 4, N), nw waves per block.
 hipError_t launch_attention16(int nw, int x1, const float* qkv, float* out, int L, int C, int N, hipStream_t st);
-void launch_attention_f32(int D, int qt, const float* qkv, float* out, int L, int C, dim3 grid, hipStream_t st);
+void launch_attention_f32(int D, int qt, const float* qkv, float* out, int L, int C, dim3 grid, hipStream_t st,
+                          float* stats = nullptr);
 // fused attention-block token kernels (tokmlp.h), k_tok.hip.
 void launch_tok_qkv_lds(int C, int tpb, int x1, const TokParams& tp, dim3 grid, hipStream_t st);
 // C = 256 QKV with 8-wave blocks of 64 tokens x 384 columns (tok_ln_qkv_w_kernel); grid (M / 64, 2).

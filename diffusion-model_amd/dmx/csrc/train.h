@@ -39,8 +39,7 @@ struct GnBwdParams {
   float* dr;             // [N][HW][C]
   float* dres;           // residual gradient dy (res != null): dres_mode 1 writes, 2 accumulates
   int dres_mode;
-  float* sums;           // [N][2]: S1, S2 (finish out)
-  float* chpart;         // [N][2][C]: per-sample dgamma, dbeta sums (finish out)
+  float* chpart;         // [N][2][C]: per-sample dgamma, dbeta sums (pass B out)
   float* demb; int demb_stride, demb_off;  // or null: demb[n][off + c] = sum over pixels of dout
   int chunks, ppb;       // pass A: blocks per sample, pixels per block
   double* bsum;          // [N][chunks][2] block partials of S1, S2
@@ -92,7 +91,7 @@ DMX_DEV float gn_dy(const GnBwdParams& p, size_t idx, int c, float xh, float& dr
 // Pass A, grid (chunks, N): block b of sample n takes pixels [b ppb, (b + 1) ppb).  Thread ->
 // (channels, pixels) ownership: C >= 256: channels tid + 256 q (q < C / 256), every pixel;
 // C < 256 (C | 256): channel tid % C, pixels tid / C + k (256 / C).  Coalesced rows.  Block
-// partials are combined in a fixed order by gn_bwd_finish_kernel.
+// partials are combined in a fixed order by gn_bwd_apply_kernel.
 static __global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const GnBwdParams p) {
   __shared__ double red[8];
   __shared__ float tg[3][2][256];
@@ -167,38 +166,46 @@ static __global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const GnBwdPa
   }
 }
 
-// Block partials -> per-sample S1, S2, dgamma / dbeta rows and the emb gradient (chunk order).
-static __global__ __launch_bounds__(256) void gn_bwd_finish_kernel(const GnBwdParams p) {
-  const int n = blockIdx.x, tid = threadIdx.x;
-  if (tid == 0) {
+// Pass B, grid (achunks, N): the block partials of pass A -> per-sample S1, S2 (wave 0: lanes over the
+// chunks in double, then a fixed shuffle tree), block 0 of each sample also writes the dgamma / dbeta
+// rows and the emb gradient (chunk order); then dr = rstd (gamma dy - S1/cnt - xhat S2/cnt), dres.
+static __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const GnBwdParams p) {
+  __shared__ double red[8];
+  __shared__ float s12[2];
+  const int n = blockIdx.y, tid = threadIdx.x;
+  if (tid < 64) {
     double a = 0.0, b = 0.0;
-    for (int k = 0; k < p.chunks; ++k) {
+    for (int k = tid; k < p.chunks; k += 64) {
       a += p.bsum[2 * ((size_t)n * p.chunks + k)];
       b += p.bsum[2 * ((size_t)n * p.chunks + k) + 1];
     }
-    p.sums[2 * n] = (float)a;
-    p.sums[2 * n + 1] = (float)b;
-  }
-  for (int c = tid; c < p.C; c += 256) {
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-    for (int k = 0; k < p.chunks; ++k) {
-      const float* o = p.bch + ((size_t)n * p.chunks + k) * 3 * p.C;
-      a0 += o[c];
-      a1 += o[p.C + c];
-      a2 += o[2 * p.C + c];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      a += __shfl_xor(a, o, 64);
+      b += __shfl_xor(b, o, 64);
     }
-    p.chpart[((size_t)n * 2 + 0) * p.C + c] = a0;
-    p.chpart[((size_t)n * 2 + 1) * p.C + c] = a1;
-    if (p.demb != nullptr) p.demb[(size_t)n * p.demb_stride + p.demb_off + c] = a2;
+    if (tid == 0) {
+      s12[0] = (float)a;
+      s12[1] = (float)b;
+    }
   }
-}
-
-static __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const GnBwdParams p) {
-  __shared__ double red[8];
-  const int n = blockIdx.y, tid = threadIdx.x;
-  const float2 st = gn_stats_from_rowpart(p, n, red);
+  if (blockIdx.x == 0) {
+    for (int c = tid; c < p.C; c += 256) {
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+      for (int k = 0; k < p.chunks; ++k) {
+        const float* o = p.bch + ((size_t)n * p.chunks + k) * 3 * p.C;
+        a0 += o[c];
+        a1 += o[p.C + c];
+        a2 += o[2 * p.C + c];
+      }
+      p.chpart[((size_t)n * 2 + 0) * p.C + c] = a0;
+      p.chpart[((size_t)n * 2 + 1) * p.C + c] = a1;
+      if (p.demb != nullptr) p.demb[(size_t)n * p.demb_stride + p.demb_off + c] = a2;
+    }
+  }
+  const float2 st = gn_stats_from_rowpart(p, n, red);  // (its barriers also publish s12)
   const float cnt = (float)p.HW * (float)p.C;
-  const float m1 = p.sums[2 * n] / cnt, m2 = p.sums[2 * n + 1] / cnt;
+  const float m1 = s12[0] / cnt, m2 = s12[1] / cnt;
   const size_t base = (size_t)n * p.HW * p.C;
   const int per = p.HW * p.C;
   for (int i = blockIdx.x * 256 + tid; i < per; i += gridDim.x * 256) {
@@ -536,18 +543,35 @@ static __global__ __launch_bounds__(256) void wgrad_x3_kernel(const WgradParams 
     }
 }
 
-// grad (torch layout) = sum over splits (split order); k = tap * Cin + ci -> [co][ci][tap]
-// (input channels >= cin_real — the zero padding of a 3-channel input — are dropped).
-static __global__ void wgrad_finish_kernel(const float* part, int splits, int Cout, int Cin, int cin_real, int taps,
-                                           float* grad) {
+// grad (torch layout) = sum over the split slabs; k = tap * Cin + ci -> [co][ci][tap] (input channels
+// >= cin_real — the zero padding of a 3-channel input — are dropped).  64 consecutive elements per
+// block, the slabs split over 4 row groups (slab z to group z % 4, four independent load chains per
+// thread) and the groups added in a fixed order: deterministic, and ~4x the loads in flight of one
+// thread walking all slabs (which left this kernel latency-bound at Cout K / 256 blocks).
+static __global__ __launch_bounds__(256) void wgrad_finish_kernel(const float* part, int splits, int Cout, int Cin,
+                                                                  int cin_real, int taps, float* grad) {
+  __shared__ float red[4][64];
   const int K = taps * Cin;
   const size_t total = (size_t)Cout * K;
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
-    const int co = (int)(i / K), k = (int)(i % K), tap = k / Cin, ci = k - tap * Cin;
-    if (ci >= cin_real) continue;
-    float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += part[(size_t)z * total + i];
-    grad[((size_t)co * cin_real + ci) * taps + tap] = s;
+  const int cl = threadIdx.x & 63, zg = threadIdx.x >> 6;
+  const size_t i = (size_t)blockIdx.x * 64 + cl;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (i < total) {
+    int z = zg;
+    for (; z + 12 < splits; z += 16) {
+      s0 += part[(size_t)z * total + i];
+      s1 += part[(size_t)(z + 4) * total + i];
+      s2 += part[(size_t)(z + 8) * total + i];
+      s3 += part[(size_t)(z + 12) * total + i];
+    }
+    for (; z < splits; z += 4) s0 += part[(size_t)z * total + i];
+  }
+  red[zg][cl] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (zg == 0 && i < total) {
+    const int co = (int)(i / K), k = (int)(i - (size_t)co * K), tap = k / Cin, ci = k - tap * Cin;
+    if (ci < cin_real)
+      grad[((size_t)co * cin_real + ci) * taps + tap] = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
   }
 }
 
@@ -650,225 +674,254 @@ static __global__ void upcat_bwd_kernel(const float* dcat, float* dskip, float* 
 }
 
 // ---------------------------------------------------------------------------
-// Multi-head attention core backward (fp32), per (sample, head):
-//   P = softmax(Q K^T / sqrt D), O = P V;  given dO:
+// Multi-head attention core backward on the fp32 matrix cores (v_mfma_f32_16x16x4f32), per
+// (sample, head):  P = softmax(Q K^T / sqrt D), O = P V;  given dO:
 //   Dlt_i = sum_d dO_i O_i;  dS = P (dO V^T - Dlt);  dQ = dS K / sqrt D;  dK = dS^T Q / sqrt D;  dV = P^T dO.
-// attn_rowstats_kernel: per query row max m_i, sum l_i of exp(s - m) and Dlt_i (one thread per row).
-// attn_dq_kernel: one thread per query row, keys streamed through LDS in 64-key tiles.
-// attn_dkv_kernel: one thread per key, queries streamed through LDS.
-// qkv: [N][L][3C] (q | k | v, head h at columns h*D), o / dO: [N][L][C]; dqkv: [N][L][3C].
+// P is recomputed from Q, K and the per-query (max m_i, 1 / sum l_i); nothing L x L is stored.
+//   attn_dq_mfma_kernel: 64 queries per block, 16 per wave with the query on the lane.  m_i and 1 / l_i
+//     come from the training forward (kernels.h attention_kernel writes them to st), or with STATS
+//     from a first pass over the keys (online); Dlt_i goes to st.  Then it streams K and V:
+//     S^T = K Q^T,  dP^T = V dO^T,  dS^T = P^T (dP^T - Dlt),  dQ^T += K^T dS^T.
+//   attn_dkv_mfma_kernel (after it): 64 keys per block, the key on the lane, queries streamed:
+//     S = Q K^T,  dP = dO V^T,  dV^T += dO^T P,  dK^T += Q^T dS.
+// The 16 x 16 accumulator of one product (lane: column lane % 16, rows 4 (lane / 16) + r) is the B
+// operand of the next, contracting over its rows: step r maps k = lane / 16 to row 4 (lane / 16) + r,
+// and the A operand is read from LDS with the same mapping (the forward kernel's arrangement,
+// kernels.h attention_kernel).  The D-contractions map d = (lane / 16) D/4 + s (contiguous float4 LDS
+// reads).  Deterministic: no atomics, fixed summation order.
+// qkv: [N][L][3C] (q | k | v, head h at columns h*D), o / dO: [N][L][C]; dqkv: [N][L][3C];
+// st: [N][4][L][3].
 // ---------------------------------------------------------------------------
-// KS waves per block split the streamed dimension (keys for rowstats / dq, queries for dkv):
-// wave w stages and walks tiles w, w + KS, ... in its own LDS slice, and the per-wave partial
-// results are combined in wave order at the end (deterministic).  KS = 1 is one wave per row
-// block; KS = 4 gives the GPU 4x the waves for the small per-(sample, head) grids of training.
-template <int D, int KS>
-__global__ __launch_bounds__(64 * KS) void attn_rowstats_kernel(const float* qkv, const float* o, const float* dout,
-                                                                float* st, int L, int C) {
-  __shared__ float ks[KS][64][D];
-  __shared__ float red[KS][64][2];
-  const int w = threadIdx.x >> 6, lt = threadIdx.x & 63;
-  const int hd = blockIdx.y, n = blockIdx.z, i = blockIdx.x * 64 + lt;
+template <int D, bool STATS>
+__global__ __launch_bounds__(256) void attn_dq_mfma_kernel(const float* qkv, const float* o, const float* dout,
+                                                           float* st, float* dqkv, int L, int C) {
+  constexpr int KC = 64, PT = D + 4, DP = D / 4, NT = D / 16;
+  __shared__ __attribute__((aligned(16))) float Ks[KC][PT];
+  __shared__ __attribute__((aligned(16))) float Vs[KC][PT];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, ql = lane & 15, g = lane >> 4;
+  const int hd = blockIdx.y, n = blockIdx.z;
+  const int qi = blockIdx.x * 64 + w * 16 + ql, qc = min(qi, L - 1);
   const size_t rs = 3 * (size_t)C;
   const float* base = qkv + (size_t)n * L * rs;
   const float sc = 1.0f / sqrtf((float)D);
-  float q[D];
+  float qf[DP], gf[DP];
+  float dl = 0.f;
+  {
+    const float* qr = base + (size_t)qc * rs + hd * D + g * DP;
+    const size_t ob = ((size_t)n * L + qc) * C + hd * D + g * DP;
 #pragma unroll
-  for (int d = 0; d < D; ++d) q[d] = i < L ? base[(size_t)i * rs + hd * D + d] * sc : 0.f;
-  float m = -INFINITY, l = 0.f;
-  const int nt = (L + 63) / 64;
-  for (int t = w; t < nt; t += KS) {
-    const int j0 = t * 64;
-    __builtin_amdgcn_wave_barrier();
-    for (int e = lt; e < 64 * D; e += 64) {
-      const int j = e / D, d = e % D;
-      ks[w][j][d] = j0 + j < L ? base[(size_t)(j0 + j) * rs + C + hd * D + d] : 0.f;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    for (int j = 0; j < 64 && j0 + j < L; ++j) {
-      float s = 0.f;
+    for (int s = 0; s < DP; s += 4) {
+      const floatx4 q4 = ld4(qr + s), g4 = ld4(dout + ob + s), o4 = ld4(o + ob + s);
 #pragma unroll
-      for (int d = 0; d < D; ++d) s += q[d] * ks[w][j][d];
-      if (s > m) {
-        l = l * expf(m - s) + 1.f;
-        m = s;
-      } else {
-        l += expf(s - m);
+      for (int e = 0; e < 4; ++e) {
+        qf[s + e] = q4[e] * sc;
+        gf[s + e] = g4[e];
+        dl += g4[e] * o4[e];
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   }
-  red[w][lt][0] = m;
-  red[w][lt][1] = l;
-  __syncthreads();
-  if (w == 0 && i < L) {
-    float M = red[0][lt][0];
-#pragma unroll
-    for (int u = 1; u < KS; ++u) M = fmaxf(M, red[u][lt][0]);
-    float Ls = 0.f;
-#pragma unroll
-    for (int u = 0; u < KS; ++u) {
-      const float mu = red[u][lt][0];
-      if (mu > -INFINITY) Ls += red[u][lt][1] * expf(mu - M);
+  dl += __shfl_xor(dl, 16, 64);
+  dl += __shfl_xor(dl, 32, 64);
+  auto stage = [&](int c0, bool with_v) {
+    for (int i = tid; i < KC * (D / 4); i += 256) {
+      const int key = i / (D / 4), d4 = (i % (D / 4)) * 4;
+      floatx4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
+      if (c0 + key < L) {
+        const float* r = base + (size_t)(c0 + key) * rs + C + hd * D + d4;
+        kv = ld4(r);
+        if (with_v) vv = ld4(r + C);
+      }
+      *reinterpret_cast<floatx4*>(&Ks[key][d4]) = kv;
+      if (with_v) *reinterpret_cast<floatx4*>(&Vs[key][d4]) = vv;
     }
-    float dl = 0.f;
-    const size_t ob = ((size_t)n * L + i) * C + hd * D;
+  };
+  auto dotk = [&](const float (*X)[PT], int row, const float* f) {  // 16 x 16 tile of X Q^T-like products
+    floatx4 a = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int d = 0; d < D; ++d) dl += dout[ob + d] * o[ob + d];
-    float* so = st + (((size_t)n * 4 + hd) * L + i) * 3;
-    so[0] = M;
-    so[1] = Ls;
-    so[2] = dl;
+    for (int s = 0; s < DP; s += 4) {
+      const floatx4 x4 = *reinterpret_cast<const floatx4*>(&X[row][g * DP + s]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a = __builtin_amdgcn_mfma_f32_16x16x4f32(x4[e], f[s + e], a, 0, 0, 0);
+    }
+    return a;
+  };
+  const int nch = (L + KC - 1) / KC;
+  float M, il;
+  float* so = st + (((size_t)n * 4 + hd) * L + qc) * 3;
+  if constexpr (STATS) {
+    // per-lane online max / sum over the lane's keys (4 of every 16), then across the 4 lane groups
+    float m = -INFINITY, l = 0.f;
+    for (int c = 0; c < nch; ++c) {
+      const int c0 = c * KC;
+      stage(c0, false);
+      __syncthreads();
+#pragma unroll
+      for (int kt = 0; kt < KC / 16; ++kt) {
+        if (c0 + kt * 16 >= L) break;
+        const floatx4 s4 = dotk(Ks, kt * 16 + ql, qf);
+        float mx = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (c0 + kt * 16 + 4 * g + r < L) mx = fmaxf(mx, s4[r]);
+        if (mx > -INFINITY) {
+          const float mn = fmaxf(m, mx);
+          float a = l * __expf(m - mn);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (c0 + kt * 16 + 4 * g + r < L) a += __expf(s4[r] - mn);
+          l = a;
+          m = mn;
+        }
+      }
+      __syncthreads();
+    }
+    M = fmaxf(m, __shfl_xor(m, 16, 64));
+    M = fmaxf(M, __shfl_xor(M, 32, 64));
+    float Ls = m > -INFINITY ? l * __expf(m - M) : 0.f;
+    Ls += __shfl_xor(Ls, 16, 64);
+    Ls += __shfl_xor(Ls, 32, 64);
+    il = 1.0f / Ls;
+    if (g == 0 && qi < L) {
+      so[0] = M;
+      so[1] = il;
+    }
+  } else {
+    M = so[0];
+    il = so[1];
+  }
+  if (g == 0 && qi < L) so[2] = dl;
+  // pass 2: dQ^T (D x 16 queries per wave) += K^T dS^T over the key tiles
+  floatx4 dq[NT];
+#pragma unroll
+  for (int dt = 0; dt < NT; ++dt) dq[dt] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < nch; ++c) {
+    const int c0 = c * KC;
+    stage(c0, true);
+    __syncthreads();
+#pragma unroll
+    for (int kt = 0; kt < KC / 16; ++kt) {
+      if (c0 + kt * 16 >= L) break;
+      const floatx4 s4 = dotk(Ks, kt * 16 + ql, qf);  // S^T: keys 4g + r, query ql
+      const floatx4 p4 = dotk(Vs, kt * 16 + ql, gf);  // dP^T
+      float ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pr = c0 + kt * 16 + 4 * g + r < L ? __expf(s4[r] - M) * il : 0.f;
+        ds[r] = pr * (p4[r] - dl);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int dt = 0; dt < NT; ++dt)
+          dq[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Ks[kt * 16 + 4 * g + r][dt * 16 + ql], ds[r], dq[dt], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  if (qi < L) {  // dQ^T tile dt: lane column = query ql, rows d = dt * 16 + 4g + r
+    float* dst = dqkv + ((size_t)n * L + qi) * rs + hd * D;
+#pragma unroll
+    for (int dt = 0; dt < NT; ++dt) {
+      floatx4 v = dq[dt];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] *= sc;
+      *reinterpret_cast<floatx4*>(dst + dt * 16 + 4 * g) = v;
+    }
   }
 }
 
-template <int D, int KS>
-__global__ __launch_bounds__(64 * KS) void attn_dq_kernel(const float* qkv, const float* dout, const float* st,
-                                                          float* dqkv, int L, int C) {
-  __shared__ float ks[KS][64][D], vs[KS][64][D];
-  const int w = threadIdx.x >> 6, lt = threadIdx.x & 63;
-  const int hd = blockIdx.y, n = blockIdx.z, i = blockIdx.x * 64 + lt;
+template <int D>
+__global__ __launch_bounds__(256) void attn_dkv_mfma_kernel(const float* qkv, const float* dout, const float* st,
+                                                            float* dqkv, int L, int C) {
+  constexpr int QC = 64, PT = D + 4, DP = D / 4, NT = D / 16;
+  __shared__ __attribute__((aligned(16))) float Qs[QC][PT];
+  __shared__ __attribute__((aligned(16))) float Gs[QC][PT];
+  __shared__ __attribute__((aligned(16))) float Sm[QC], Si[QC], Sd[QC];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, ql = lane & 15, g = lane >> 4;
+  const int hd = blockIdx.y, n = blockIdx.z;
+  const int kj = blockIdx.x * 64 + w * 16 + ql, kc = min(kj, L - 1);
   const size_t rs = 3 * (size_t)C;
   const float* base = qkv + (size_t)n * L * rs;
+  const float* sth = st + ((size_t)n * 4 + hd) * L * 3;
   const float sc = 1.0f / sqrtf((float)D);
-  float q[D], g[D], dq[D];
-  const size_t ob = ((size_t)n * L + min(i, L - 1)) * C + hd * D;
+  float kf[DP], vf[DP];
+  {
+    const float* kr = base + (size_t)kc * rs + C + hd * D + g * DP;
 #pragma unroll
-  for (int d = 0; d < D; ++d) {
-    q[d] = i < L ? base[(size_t)i * rs + hd * D + d] * sc : 0.f;
-    g[d] = i < L ? dout[ob + d] : 0.f;
-    dq[d] = 0.f;
-  }
-  const float* s3 = st + (((size_t)n * 4 + hd) * L + min(i, L - 1)) * 3;
-  const float m = s3[0], il = 1.0f / s3[1], dl = s3[2];
-  const int nt = (L + 63) / 64;
-  for (int t = w; t < nt; t += KS) {
-    const int j0 = t * 64;
-    __builtin_amdgcn_wave_barrier();
-    for (int e = lt; e < 64 * D; e += 64) {
-      const int j = e / D, d = e % D;
-      const bool ok = j0 + j < L;
-      ks[w][j][d] = ok ? base[(size_t)(j0 + j) * rs + C + hd * D + d] : 0.f;
-      vs[w][j][d] = ok ? base[(size_t)(j0 + j) * rs + 2 * C + hd * D + d] : 0.f;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    for (int j = 0; j < 64 && j0 + j < L; ++j) {
-      float s = 0.f, dp = 0.f;
+    for (int s = 0; s < DP; s += 4) {
+      const floatx4 k4 = ld4(kr + s), v4 = ld4(kr + C + s);
 #pragma unroll
-      for (int d = 0; d < D; ++d) {
-        s += q[d] * ks[w][j][d];
-        dp += g[d] * vs[w][j][d];
-      }
-      const float ds = expf(s - m) * il * (dp - dl);
-#pragma unroll
-      for (int d = 0; d < D; ++d) dq[d] += ds * ks[w][j][d];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  }
-  if constexpr (KS > 1) {  // combine the waves' partial dQ in wave order (reuse the K slices)
-    __syncthreads();
-    float* red = &ks[0][0][0];  // [KS][64][D] floats
-#pragma unroll
-    for (int d = 0; d < D; ++d) red[(w * 64 + lt) * D + d] = dq[d];
-    __syncthreads();
-    if (w != 0) return;
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      float a = red[lt * D + d];
-#pragma unroll
-      for (int u = 1; u < KS; ++u) a += red[(u * 64 + lt) * D + d];
-      dq[d] = a;
-    }
-  }
-  if (i < L) {
-    float* dst = dqkv + ((size_t)n * L + i) * rs + hd * D;
-#pragma unroll
-    for (int d = 0; d < D; ++d) dst[d] = dq[d] * sc;
-  }
-}
-
-template <int D, int KS>
-__global__ __launch_bounds__(64 * KS) void attn_dkv_kernel(const float* qkv, const float* dout, const float* st,
-                                                           float* dqkv, int L, int C) {
-  __shared__ float qs[KS][64][D], gs[KS][64][D], ss[KS][64][3];
-  const int w = threadIdx.x >> 6, lt = threadIdx.x & 63;
-  const int hd = blockIdx.y, n = blockIdx.z, j = blockIdx.x * 64 + lt;
-  const size_t rs = 3 * (size_t)C;
-  const float* base = qkv + (size_t)n * L * rs;
-  const float sc = 1.0f / sqrtf((float)D);
-  float k[D], v[D], dk[D], dv[D];
-#pragma unroll
-  for (int d = 0; d < D; ++d) {
-    k[d] = j < L ? base[(size_t)j * rs + C + hd * D + d] : 0.f;
-    v[d] = j < L ? base[(size_t)j * rs + 2 * C + hd * D + d] : 0.f;
-    dk[d] = dv[d] = 0.f;
-  }
-  const int nt = (L + 63) / 64;
-  for (int t = w; t < nt; t += KS) {
-    const int i0 = t * 64;
-    __builtin_amdgcn_wave_barrier();
-    for (int e = lt; e < 64 * D; e += 64) {
-      const int i = e / D, d = e % D;
-      const bool ok = i0 + i < L;
-      qs[w][i][d] = ok ? base[(size_t)(i0 + i) * rs + hd * D + d] * sc : 0.f;
-      gs[w][i][d] = ok ? dout[((size_t)n * L + i0 + i) * C + hd * D + d] : 0.f;
-    }
-    if (i0 + lt < L) {
-      const float* s3 = st + (((size_t)n * 4 + hd) * L + i0 + lt) * 3;
-      ss[w][lt][0] = s3[0];
-      ss[w][lt][1] = 1.0f / s3[1];
-      ss[w][lt][2] = s3[2];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    for (int i = 0; i < 64 && i0 + i < L; ++i) {
-      float s = 0.f, dp = 0.f;
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        s += qs[w][i][d] * k[d];
-        dp += gs[w][i][d] * v[d];
-      }
-      const float pr = expf(s - ss[w][i][0]) * ss[w][i][1];
-      const float ds = pr * (dp - ss[w][i][2]);
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        dv[d] += pr * gs[w][i][d];
-        dk[d] += ds * qs[w][i][d];  // qs already carries the 1/sqrt(D)
+      for (int e = 0; e < 4; ++e) {
+        kf[s + e] = k4[e];
+        vf[s + e] = v4[e];
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   }
-  if constexpr (KS > 1) {  // combine the waves' partial dK / dV in wave order
-    __syncthreads();
-    float* rk = &qs[0][0][0];
-    float* rv = &gs[0][0][0];
+  floatx4 dk[NT], dv[NT];
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
-      rk[(w * 64 + lt) * D + d] = dk[d];
-      rv[(w * 64 + lt) * D + d] = dv[d];
-    }
-    __syncthreads();
-    if (w != 0) return;
+  for (int dt = 0; dt < NT; ++dt) dk[dt] = dv[dt] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int nch = (L + QC - 1) / QC;
+  for (int c = 0; c < nch; ++c) {
+    const int c0 = c * QC;
+    // queries past L: zero Q / dO rows and 1 / l = 0, so P = dS = 0 there
+    for (int i = tid; i < QC * (D / 4); i += 256) {
+      const int q = i / (D / 4), d4 = (i % (D / 4)) * 4;
+      floatx4 qv = {0.f, 0.f, 0.f, 0.f}, gv = {0.f, 0.f, 0.f, 0.f};
+      if (c0 + q < L) {
+        qv = ld4(base + (size_t)(c0 + q) * rs + hd * D + d4);
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
-      float a = rk[lt * D + d], b = rv[lt * D + d];
-#pragma unroll
-      for (int u = 1; u < KS; ++u) {
-        a += rk[(u * 64 + lt) * D + d];
-        b += rv[(u * 64 + lt) * D + d];
+        for (int e = 0; e < 4; ++e) qv[e] *= sc;
+        gv = ld4(dout + ((size_t)n * L + c0 + q) * C + hd * D + d4);
       }
-      dk[d] = a;
-      dv[d] = b;
+      *reinterpret_cast<floatx4*>(&Qs[q][d4]) = qv;
+      *reinterpret_cast<floatx4*>(&Gs[q][d4]) = gv;
     }
-  }
-  if (j < L) {
-    float* dst = dqkv + ((size_t)n * L + j) * rs + hd * D;
+    if (tid < QC) {
+      const bool ok = c0 + tid < L;
+      Sm[tid] = ok ? sth[(size_t)(c0 + tid) * 3] : 0.f;
+      Si[tid] = ok ? sth[(size_t)(c0 + tid) * 3 + 1] : 0.f;
+      Sd[tid] = ok ? sth[(size_t)(c0 + tid) * 3 + 2] : 0.f;
+    }
+    __syncthreads();
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
-      dst[C + d] = dk[d];
-      dst[2 * C + d] = dv[d];
+    for (int qt = 0; qt < QC / 16; ++qt) {
+      if (c0 + qt * 16 >= L) break;
+      floatx4 s4 = {0.f, 0.f, 0.f, 0.f}, p4 = {0.f, 0.f, 0.f, 0.f};  // S, dP: queries 4g + r, key ql
+#pragma unroll
+      for (int s = 0; s < DP; s += 4) {
+        const floatx4 q4 = *reinterpret_cast<const floatx4*>(&Qs[qt * 16 + ql][g * DP + s]);
+        const floatx4 g4 = *reinterpret_cast<const floatx4*>(&Gs[qt * 16 + ql][g * DP + s]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s4 = __builtin_amdgcn_mfma_f32_16x16x4f32(q4[e], kf[s + e], s4, 0, 0, 0);
+          p4 = __builtin_amdgcn_mfma_f32_16x16x4f32(g4[e], vf[s + e], p4, 0, 0, 0);
+        }
+      }
+      const int q0 = qt * 16 + 4 * g;
+      const floatx4 mq = *reinterpret_cast<const floatx4*>(&Sm[q0]);
+      const floatx4 iq = *reinterpret_cast<const floatx4*>(&Si[q0]);
+      const floatx4 dq = *reinterpret_cast<const floatx4*>(&Sd[q0]);
+      float pr[4], ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pr[r] = __expf(s4[r] - mq[r]) * iq[r];
+        ds[r] = pr[r] * (p4[r] - dq[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int dt = 0; dt < NT; ++dt) {
+          dv[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Gs[q0 + r][dt * 16 + ql], pr[r], dv[dt], 0, 0, 0);
+          dk[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(Qs[q0 + r][dt * 16 + ql], ds[r], dk[dt], 0, 0, 0);
+        }
+    }
+    __syncthreads();
+  }
+  if (kj < L) {  // dK^T / dV^T tile dt: lane column = key ql, rows d = dt * 16 + 4g + r (Qs carries 1/sqrt D)
+    float* dst = dqkv + ((size_t)n * L + kj) * rs + hd * D;
+#pragma unroll
+    for (int dt = 0; dt < NT; ++dt) {
+      *reinterpret_cast<floatx4*>(dst + C + dt * 16 + 4 * g) = dk[dt];
+      *reinterpret_cast<floatx4*>(dst + 2 * C + dt * 16 + 4 * g) = dv[dt];
     }
   }
 }

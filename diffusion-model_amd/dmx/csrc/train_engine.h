@@ -34,6 +34,7 @@ struct TAttn {  // one AttenionBlock (models/unet_cond.py:32-52)
   const float* x = nullptr;
   float *xl = nullptr, *qkv = nullptr, *ao = nullptr, *av = nullptr, *al = nullptr, *h1 = nullptr, *f = nullptr,
         *out = nullptr;
+  float* st = nullptr;  // [N][4][L][3]: the forward's row max, 1 / sum (attention_kernel), the backward's Dlt
 };
 struct TUp {  // Up's bilinear x2 + pad + concat input (models/unet_cond.py:87-97)
   float* cat = nullptr;
@@ -273,9 +274,10 @@ static TAttn train_attn(Run& R, const AttnW& a, const float* x, int N, int H, in
   t.h1 = R.ws.get<float>((size_t)M * C);
   t.f = R.ws.get<float>((size_t)M * C);
   t.out = R.ws.get<float>((size_t)M * C);
+  t.st = R.ws.get<float>((size_t)N * 4 * L * 3);
   layernorm(R, x, t.xl, a.l1w, a.l1b, M, C);
   gemm(R, plain_src(t.xl, C), SRC_PLAIN, N, H, W, a.qkv, EPI_BIAS, t.qkv, nullptr, nullptr, 1);
-  attention_core(R, t.qkv, t.ao, N, L, C);
+  attention_core(R, t.qkv, t.ao, N, L, C, t.st);
   gemm(R, plain_src(t.ao, C), SRC_PLAIN, N, H, W, a.o, EPI_BIAS_RES, t.av, t.xl, nullptr, 1);
   layernorm(R, t.av, t.al, a.l2w, a.l2b, M, C);
   gemm(R, plain_src(t.al, C), SRC_PLAIN, N, H, W, a.f1, EPI_BIAS, t.h1, nullptr, nullptr, 1);
@@ -551,7 +553,7 @@ static void wgrad(Run& R, const float* dy, const float* x, int N, int H, int W, 
     else wgrad_kernel<<<dim3(cdiv(Cout, 64), cdiv(K, 64), splits), 256, 0, R.st>>>(p);
     R.end();
     HIPCHK(hipGetLastError());
-    wgrad_finish_kernel<<<ew_blocks((size_t)Cout * K), 256, 0, R.st>>>(part, splits, Cout, Cin, cin_real, taps, grad);
+    wgrad_finish_kernel<<<(int)(((size_t)Cout * K + 63) / 64), 256, 0, R.st>>>(part, splits, Cout, Cin, cin_real, taps, grad);
     HIPCHK(hipGetLastError());
   }
   // bias gradient = column sums of dY: the fast kernel's per-split sums, else a pass over dY
@@ -585,7 +587,7 @@ static void dgrad(Run& R, const float* dy, int Cy, int N, int H, int W, const Co
 
 static void gn_bwd_launch(Run& R, const float* r, const float2* rp, int nseg, int rrows, const Vec& g, const Vec& b,
                           const float* res, int act, const float* dout, int N, int C, int HW, float* dr, float* dres,
-                          int dres_mode, float* sums, float* chpart, float* demb, int demb_stride, int demb_off,
+                          int dres_mode, float* chpart, float* demb, int demb_stride, int demb_off,
                           int ppb, double* bsum, float* bch);
 
 static void gn_bwd(Run& R, const float* r, const float2* rp, int nseg, int rrows, const Vec& g, const Vec& b,
@@ -594,18 +596,17 @@ static void gn_bwd(Run& R, const float* r, const float2* rp, int nseg, int rrows
   // pass A over ~512 blocks in total (>= 16 pixels each)
   const int chunks = std::max(1, std::min(cdiv(512, N), cdiv(HW, 16)));
   const int ppb = cdiv(HW, chunks);
-  float* sums = R.ws.get<float>((size_t)2 * N);
   float* chpart = R.ws.get<float>((size_t)N * 2 * C);
   double* bsum = R.ws.get<double>((size_t)N * chunks * 2);
   float* bch = R.ws.get<float>((size_t)N * chunks * 3 * C);
-  if (!R.plan) gn_bwd_launch(R, r, rp, nseg, rrows, g, b, res, act, dout, N, C, HW, dr, dres, dres_mode, sums, chpart,
+  if (!R.plan) gn_bwd_launch(R, r, rp, nseg, rrows, g, b, res, act, dout, N, C, HW, dr, dres, dres_mode, chpart,
                              demb, demb_stride, demb_off, ppb, bsum, bch);
   colsum_pair(R, chpart, N, C, 2 * (size_t)C, ggamma, gbeta);
 }
 
 static void gn_bwd_launch(Run& R, const float* r, const float2* rp, int nseg, int rrows, const Vec& g, const Vec& b,
                           const float* res, int act, const float* dout, int N, int C, int HW, float* dr, float* dres,
-                          int dres_mode, float* sums, float* chpart, float* demb, int demb_stride, int demb_off,
+                          int dres_mode, float* chpart, float* demb, int demb_stride, int demb_off,
                           int ppb, double* bsum, float* bch) {
   GnBwdParams p;
   std::memset(&p, 0, sizeof(p));
@@ -623,7 +624,6 @@ static void gn_bwd_launch(Run& R, const float* r, const float2* rp, int nseg, in
   p.dr = dr;
   p.dres = dres;
   p.dres_mode = dres_mode;
-  p.sums = sums;
   p.chpart = chpart;
   p.demb = demb;
   p.demb_stride = demb_stride;
@@ -634,7 +634,6 @@ static void gn_bwd_launch(Run& R, const float* r, const float2* rp, int nseg, in
   p.bch = bch;
   R.begin("gn_bwd_reduce_kernel", 0.0, 4.0 * (double)N * HW * C * (res ? 3 : 2));
   gn_bwd_reduce_kernel<<<dim3(p.chunks, N), 256, 0, R.st>>>(p);
-  gn_bwd_finish_kernel<<<N, 256, 0, R.st>>>(p);
   R.end();
   HIPCHK(hipGetLastError());
   const int achunks = std::max(1, std::min(64, cdiv(HW * C, 4096)));
@@ -662,30 +661,34 @@ static void ln_bwd(Run& R, const float* x, const Vec& w, const float* dy, float*
   colsum_pair(R, part, blocks, C, 2 * (size_t)C, gw, gb);
 }
 
-static void attn_core_bwd(Run& R, const float* qkv, const float* o, const float* dout, float* dqkv, int N, int L,
-                          int C) {
-  float* st = R.ws.get<float>((size_t)N * 4 * L * 3);
-  if (R.plan) return;
+// the two MFMA attention-backward launches (train.h); st: [N][4][L][3] — with have_stats, slots 0 / 1
+// hold the forward's row max and 1 / sum (attention_kernel), else the dq kernel derives them first
+static void attn_core_bwd_launch(const float* qkv, const float* o, const float* dout, float* dqkv, float* st, int N,
+                                 int L, int C, bool have_stats, hipStream_t s) {
   const int D = C / 4;
   const dim3 grid(cdiv(L, 64), 4, N);
-  R.begin("attn_bwd_kernels<" + std::to_string(D) + ">", 3.0 * 4.0 * N * (double)L * L * C, 4.0 * N * (double)L * 6 * C);
-  if (D == 16) {  // 4 waves per block split the streamed dimension (training grids are small)
-    attn_rowstats_kernel<16, 4><<<grid, 256, 0, R.st>>>(qkv, o, dout, st, L, C);
-    attn_dq_kernel<16, 4><<<grid, 256, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
-    attn_dkv_kernel<16, 4><<<grid, 256, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
-  } else if (D == 32) {
-    attn_rowstats_kernel<32, 4><<<grid, 256, 0, R.st>>>(qkv, o, dout, st, L, C);
-    attn_dq_kernel<32, 4><<<grid, 256, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
-    attn_dkv_kernel<32, 4><<<grid, 256, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
-  } else if (D == 64) {
-    attn_rowstats_kernel<64, 1><<<grid, 64, 0, R.st>>>(qkv, o, dout, st, L, C);
-    attn_dq_kernel<64, 1><<<grid, 64, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
-    attn_dkv_kernel<64, 1><<<grid, 64, 0, R.st>>>(qkv, dout, st, dqkv, L, C);
-  } else {
-    throw Error(DMX_E_INTERNAL, "attention backward: unsupported head dim");
+#define DMX_ATTB(DD)                                                                                   \
+  if (have_stats) attn_dq_mfma_kernel<DD, false><<<grid, 256, 0, s>>>(qkv, o, dout, st, dqkv, L, C);  \
+  else attn_dq_mfma_kernel<DD, true><<<grid, 256, 0, s>>>(qkv, o, dout, st, dqkv, L, C);              \
+  attn_dkv_mfma_kernel<DD><<<grid, 256, 0, s>>>(qkv, dout, st, dqkv, L, C);
+  switch (D) {
+    case 16: DMX_ATTB(16) break;
+    case 32: DMX_ATTB(32) break;
+    case 64: DMX_ATTB(64) break;
+    default: throw Error(DMX_E_INTERNAL, "attention backward: unsupported head dim");
   }
-  R.end();
+#undef DMX_ATTB
   HIPCHK(hipGetLastError());
+}
+
+// st: the training forward's statistics (TAttn::st)
+static void attn_core_bwd(Run& R, const float* qkv, const float* o, const float* dout, float* dqkv, float* st, int N,
+                          int L, int C) {
+  if (R.plan) return;
+  R.begin("attn_bwd_kernels<" + std::to_string(C / 4) + ">", 4.0 * 4.0 * N * (double)L * L * C,
+          4.0 * N * (double)L * 6 * C);
+  attn_core_bwd_launch(qkv, o, dout, dqkv, st, N, L, C, true, R.st);
+  R.end();
 }
 
 // ResBlock backward: dout -> dx (x's gradient; accumulated when dx_acc), parameter gradients,
@@ -733,7 +736,7 @@ static void attn_bwd(Run& R, const TAttn& t, const GradMap& G, float* dout, floa
   float* dao = R.ws.get<float>((size_t)M * C);
   dgrad(R, dav, C, N, H, W, a.dout, dao, false);
   float* dqkv = R.ws.get<float>((size_t)M * 3 * C);
-  attn_core_bwd(R, t.qkv, t.ao, dao, dqkv, N, L, C);
+  attn_core_bwd(R, t.qkv, t.ao, dao, dqkv, t.st, N, L, C);
   wgrad(R, dqkv, t.xl, N, H, W, C, 3 * C, 1, C, G(p + ".mha.in_proj_weight"), G(p + ".mha.in_proj_bias"));
   dgrad(R, dqkv, 3 * C, N, H, W, a.dqkv, dav, true);  // dxl = dav + in_proj^T(dqkv)
   ln_bwd(R, t.x, a.l1w, dav, dx, false, M, C, G(p + ".ln.weight"), G(p + ".ln.bias"));

@@ -212,7 +212,14 @@ int dmx_debug_enable(dmx_model* m, int on);
 int dmx_debug_num_taps(const dmx_model* m);
 int dmx_debug_tap(dmx_model* m, int i, char* name_out, int cap, int64_t* count_out, float* dst, void* stream);
 
-/* ---- timing diagnostic (libraries built with -DDMX_WSTAMP=1 only; regular builds return 0): the
+/* ---- multi-head attention core backward (the adjoint of nn.MultiheadAttention's softmax(Q K^T /
+ * sqrt(D)) V core, models/unet_cond.py:36,49, 4 heads; used by dmx_train_backward, exported for its
+ * test): qkv (n,L,3C) = q | k | v (head h at columns h*C/4), o = the core's output (n,L,C), dout =
+ * dLoss/do (n,L,C); writes dLoss/dqkv (n,L,3C).  C/4 in {16, 32, 64}; all device fp32. */
+int dmx_attn_core_backward(const float* qkv, const float* o, const float* dout, float* dqkv, int n, int L, int C,
+                           void* stream);
+
+/* ---- timing diagnostic (libraries built with -DDMX_DIAG=1 only; regular builds return 0): the
  * per-block s_memtime stamps of the Winograd conv launches ({start, after prologue, after chunk loop,
  * end, hardware id} x 2048 blocks x 32 launch slots, uint64) copied to host memory; returns the count
  * copied or -1; host == NULL resets the table and the launch counter.  tools/wino_stamps.py reads them. */
