@@ -307,7 +307,9 @@ struct dmx_model {
   // tensors, in finalize order; the f16 planes of the split GEMMs are re-derived lazily
   // (planes_stale) before the next split-precision launch.
   std::vector<std::function<void(hipStream_t)>> jobs;
-  std::vector<std::function<void(hipStream_t)>> post_jobs;  // replayed after the repacks (device splits)
+  std::vector<dmx::SplitJob> split_jobs;  // device-side splits of the training data-gradient weights,
+  void* split_table = nullptr;            // replayed batched after the repacks (two launches)
+  size_t split_table_n = 0;
   std::vector<dmx::CopyJob> copies;     // parameter copies and weight repacks, replayed batched
   std::vector<dmx::RepackJob> repacks;  // (one launch each) by dmx_model_refresh
   void* job_tables = nullptr;           // device copies of the two tables
@@ -405,13 +407,9 @@ struct Packer {
     f(st);
     m->jobs.push_back(std::move(f));
   }
-  // run now (after everything recorded so far) and on every refresh after the batched repacks
-  void post_job(std::function<void(hipStream_t)> f) {
-    f(st);
-    m->post_jobs.push_back(std::move(f));
-  }
-  // f16 hi / lo planes of a packed fp32 B with a device-side scale (no host round trip), re-derived
-  // on the device after every refresh: the training data-gradient weights (train_engine.h)
+  // f16 hi / lo planes of a packed fp32 B with a device-side scale (no host round trip), derived on
+  // the device by run_split_jobs (the end of the training pack, and every refresh after the repacks):
+  // the training data-gradient weights (train_engine.h)
   void split_dev(ConvW& c) {
     const size_t n = (size_t)c.phases * c.npad * c.kpad;
     void* h = nullptr;
@@ -421,21 +419,13 @@ struct Packer {
     m->owned.push_back(h);
     HIPCHK(hipMalloc(&l, n * sizeof(_Float16)));
     m->owned.push_back(l);
-    constexpr int NP = 64;  // partial maxima of the weight's absmax
-    HIPCHK(hipMalloc(&a, NP * sizeof(unsigned) + 64));
+    HIPCHK(hipMalloc(&a, SPLIT_PARTS * sizeof(unsigned) + 64));
     m->owned.push_back(a);
     c.Bh = static_cast<_Float16*>(h);
     c.Bl = static_cast<_Float16*>(l);
     c.amax_dev = static_cast<unsigned*>(a);
-    c.inv_dev = reinterpret_cast<float*>(static_cast<char*>(a) + NP * sizeof(unsigned));
-    const ConvW cc = c;
-    post_job([cc, n](hipStream_t s) {
-      absmax_part_kernel<<<NP, 256, 0, s>>>(cc.B, n, cc.amax_dev);
-      HIPCHK(hipGetLastError());
-      split_weights_dev_kernel<<<(int)std::min<size_t>((n + 255) / 256, 8192), 256, 0, s>>>(cc.B, cc.Bh, cc.Bl, n,
-                                                                                            cc.amax_dev, NP, cc.inv_dev);
-      HIPCHK(hipGetLastError());
-    });
+    c.inv_dev = reinterpret_cast<float*>(static_cast<char*>(a) + SPLIT_PARTS * sizeof(unsigned));
+    m->split_jobs.push_back(SplitJob{c.B, c.Bh, c.Bl, c.amax_dev, c.inv_dev, n});
   }
   float* copy(const std::string& name) {
     auto& t = in(name);
@@ -2257,6 +2247,7 @@ int dmx_model_destroy(dmx_model* m) {
     drop_graph(m);
     for (void* p : m->owned) (void)hipFree(p);
     if (m->job_tables) (void)hipFree(m->job_tables);
+    if (m->split_table) (void)hipFree(m->split_table);
     if (m->ws_mem) (void)hipFree(m->ws_mem);
     if (m->tws_mem) (void)hipFree(m->tws_mem);
     if (m->bws_mem) (void)hipFree(m->bws_mem);

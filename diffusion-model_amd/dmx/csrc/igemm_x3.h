@@ -50,7 +50,7 @@ struct X3Params {
   // Device-side operand scales (igemm_x3_kernel, fp32 A source; the training data gradients, whose dY
   // and refreshed weights have no host-known range): a_amax = bits of max|A| — A is multiplied by
   // 2^ea (max|A| 2^ea in [2^12, 2^13)) before its hi / lo split, so the lo parts stay f16-normal;
-  // w_inv = the weights' 2^-e written by split_weights_dev_kernel.  The accumulators are multiplied
+  // w_inv = the weights' 2^-e written by split_batch_kernel.  The accumulators are multiplied
   // by w_inv 2^-ea (exact: powers of two).  Null: host inv_scale, unscaled A.
   const unsigned* a_amax;     // (a_nparts > 0: a_amax holds that many per-block partial maxima)
   int a_nparts;
@@ -343,36 +343,48 @@ static __global__ void split_weights_kernel(const float* src, _Float16* hi, _Flo
 
 // Per-block partial maxima (no atomics, no zeroed slot): part[blockIdx.x] = bits of max|src| over
 // the block's grid-stride share; consumers reduce the gridDim.x partials (X3Params::a_nparts).
-static __global__ __launch_bounds__(256) void absmax_part_kernel(const float* src, size_t n, unsigned* part) {
+DMX_DEV void absmax_part_body(const float* src, size_t n, unsigned* part, unsigned bx, unsigned gx) {
   float m = 0.f;
   const size_t n4 = n / 4;
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+  for (size_t i = (size_t)bx * 256 + threadIdx.x; i < n4; i += (size_t)gx * 256) {
     const floatx4 v = reinterpret_cast<const floatx4*>(src)[i];
     m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
   }
-  for (size_t i = n4 * 4 + (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
-    m = fmaxf(m, fabsf(src[i]));
+  for (size_t i = n4 * 4 + (size_t)bx * 256 + threadIdx.x; i < n; i += (size_t)gx * 256) m = fmaxf(m, fabsf(src[i]));
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
   __shared__ float wm[4];
   if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
   __syncthreads();
-  if (threadIdx.x == 0) part[blockIdx.x] = __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3])));
+  if (threadIdx.x == 0) part[bx] = __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3])));
+}
+static __global__ __launch_bounds__(256) void absmax_part_kernel(const float* src, size_t n, unsigned* part) {
+  absmax_part_body(src, n, part, blockIdx.x, gridDim.x);
 }
 
-// Split with a device-side scale: max|w| 2^e in [2^12, 2^13) from *amax (absmax_kernel), 2^-e to *inv
-// (the training data-gradient weights, re-split on the device after every parameter refresh).
-static __global__ void split_weights_dev_kernel(const float* src, _Float16* hi, _Float16* lo, size_t n,
-                                                const unsigned* amax, int nparts, float* inv) {
-  unsigned mb = 0u;  // (absmax_part_kernel's per-block maxima)
-  for (int i = 0; i < nparts; ++i) mb = max(mb, amax[i]);
+// Split with a device-side scale: max|w| 2^e in [2^12, 2^13) from the nparts partial maxima at amax,
+// 2^-e to *inv (the training data-gradient weights, re-split on the device after every parameter
+// refresh).  Batched over the model's weights (blockIdx.y = job): absmax_batch_kernel writes
+// SPLIT_PARTS partial maxima per job, split_batch_kernel reads them and writes hi / lo.
+constexpr int SPLIT_PARTS = 64;
+struct SplitJob {
+  const float* src; _Float16* hi; _Float16* lo; unsigned* amax; float* inv; size_t n;
+};
+static __global__ __launch_bounds__(256) void absmax_batch_kernel(const SplitJob* jobs) {
+  const SplitJob j = jobs[blockIdx.y];
+  absmax_part_body(j.src, j.n, j.amax, blockIdx.x, gridDim.x);
+}
+static __global__ __launch_bounds__(256) void split_batch_kernel(const SplitJob* jobs) {
+  const SplitJob j = jobs[blockIdx.y];
+  unsigned mb = 0u;
+  for (int i = 0; i < SPLIT_PARTS; ++i) mb = max(mb, j.amax[i]);
   const int e = amax_exp(mb);
   const float scale = ldexpf(1.f, e);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *inv = ldexpf(1.f, -e);
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const float v = src[i] * scale;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *j.inv = ldexpf(1.f, -e);
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < j.n; i += (size_t)gridDim.x * blockDim.x) {
+    const float v = j.src[i] * scale;
     const _Float16 h = (_Float16)v;
-    hi[i] = h;
-    lo[i] = (_Float16)(v - (float)h);
+    j.hi[i] = h;
+    j.lo[i] = (_Float16)(v - (float)h);
   }
 }
 

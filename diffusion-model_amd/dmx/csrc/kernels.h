@@ -1034,6 +1034,12 @@ static __global__ __launch_bounds__(256) void vae_enc_tail_kernel(const float* i
 //   kind 0: Conv2d [Cout][Cin][KS][KS], k = (ky*KS+kx)*Cin + c
 //   kind 1: Linear [Cout][Cin],        k = c
 //   kind 2: ConvTranspose2d(4,s2,p1) [Cin][Cout][4][4], phase (py,px), tap (jy,jx)
+//   kind 3: data gradient of a conv3x3 pad 1 (training): src = the forward weight [Cin][Cout][3][3]
+//           (the job's Cout = the forward's input channels), B[n][tap Cin + c] = src[c][n][8 - tap]
+//           (flipped taps, channel roles swapped)
+//   kind 4: data gradient of a Linear (training): src = the forward weight [Cin][Cout], B[n][k] = src[k][n]
+// 32-bit index arithmetic (every B here holds < 2^32 elements; 64-bit divisions made the batched
+// refresh VALU-bound).
 struct RepackJob {
   float* dst; const float* src; int kind, P, Npad, Kpad, Cout, Cin, KS;
 };
@@ -1042,25 +1048,33 @@ struct CopyJob {
 };
 
 DMX_DEV void repack_range(float* dst, const float* src, int kind, int P, int Npad, int Kpad, int Cout, int Cin, int KS,
-                          size_t first, size_t stride) {
-  const size_t total = (size_t)P * Npad * Kpad;
-  for (size_t i = first; i < total; i += stride) {
-    const int k = (int)(i % Kpad), nn = (int)((i / Kpad) % Npad), ph = (int)(i / ((size_t)Kpad * Npad));
+                          unsigned first, unsigned stride) {
+  const unsigned total = (unsigned)P * (unsigned)Npad * (unsigned)Kpad, kp = (unsigned)Kpad, np = (unsigned)Npad;
+  for (unsigned i = first; i < total; i += stride) {
+    const unsigned row = i / kp;
+    const int k = (int)(i - row * kp), nn = (int)(row % np), ph = (int)(row / np);
     float v = 0.f;
     if (kind == 0) {
       if (nn < Cout && k < KS * KS * Cin) {
-        const int tap = k / Cin, c = k % Cin;
+        const int tap = k / Cin, c = k - tap * Cin;
         v = src[(((size_t)nn * Cin + c) * KS + tap / KS) * KS + tap % KS];
       }
     } else if (kind == 1) {
       if (nn < Cout && k < Cin) v = src[(size_t)nn * Cin + k];
-    } else {
+    } else if (kind == 2) {
       if (nn < Cout && k < 4 * Cin) {
         const int j = k / Cin, c = k % Cin, jy = j >> 1, jx = j & 1, py = ph >> 1, px = ph & 1;
         const int ky = py == 0 ? (jy == 0 ? 1 : 3) : (jy == 0 ? 0 : 2);
         const int kx = px == 0 ? (jx == 0 ? 1 : 3) : (jx == 0 ? 0 : 2);
         v = src[(((size_t)c * Cout + nn) * 4 + ky) * 4 + kx];
       }
+    } else if (kind == 3) {
+      if (nn < Cout && k < 9 * Cin) {
+        const int tap = k / Cin, c = k - tap * Cin;
+        v = src[((size_t)c * Cout + nn) * 9 + (8 - tap)];
+      }
+    } else {
+      if (nn < Cout && k < Cin) v = src[(size_t)k * Cout + nn];
     }
     dst[i] = v;
   }
@@ -1068,16 +1082,16 @@ DMX_DEV void repack_range(float* dst, const float* src, int kind, int P, int Npa
 
 static __global__ void repack_kernel(float* dst, const float* src, int kind, int P, int Npad, int Kpad, int Cout, int Cin,
                               int KS) {
-  repack_range(dst, src, kind, P, Npad, Kpad, Cout, Cin, KS, (size_t)blockIdx.x * blockDim.x + threadIdx.x,
-               (size_t)gridDim.x * blockDim.x);
+  repack_range(dst, src, kind, P, Npad, Kpad, Cout, Cin, KS, blockIdx.x * blockDim.x + threadIdx.x,
+               gridDim.x * blockDim.x);
 }
 
 // dmx_model_refresh: every weight repack (blockIdx.y = job) / parameter copy of the model in one
 // launch each instead of one launch per tensor (the refresh follows every optimizer step).
 static __global__ void repack_batch_kernel(const RepackJob* jobs) {
   const RepackJob j = jobs[blockIdx.y];
-  repack_range(j.dst, j.src, j.kind, j.P, j.Npad, j.Kpad, j.Cout, j.Cin, j.KS, (size_t)blockIdx.x * blockDim.x + threadIdx.x,
-               (size_t)gridDim.x * blockDim.x);
+  repack_range(j.dst, j.src, j.kind, j.P, j.Npad, j.Kpad, j.Cout, j.Cin, j.KS, blockIdx.x * blockDim.x + threadIdx.x,
+               gridDim.x * blockDim.x);
 }
 static __global__ void copy_batch_kernel(const CopyJob* jobs) {
   const CopyJob j = jobs[blockIdx.y];

@@ -126,18 +126,9 @@ static void run_arena(dmx_model* m, hipStream_t st, Arena& A, void*& mem, size_t
 // ---------------------------------------------------------------------------
 // data-gradient weights (packed once on the first training call, refreshed with the rest)
 // ---------------------------------------------------------------------------
-static __global__ void flip_transpose3x3_kernel(float* dst, const float* src, int cout, int cin) {
-  const size_t total = (size_t)cout * cin * 9;
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (size_t)gridDim.x * 256) {
-    const int t = (int)(i % 9);
-    const size_t r = i / 9;
-    const int co = (int)(r % cout), ci = (int)(r / cout);  // dst [ci][co][t] = src [co][ci][8 - t]
-    dst[i] = src[((size_t)co * cin + ci) * 9 + (8 - t)];
-  }
-}
-
 // conv3x3 pad 1 [cout][cin] -> its data gradient: conv3x3 pad 1 over dY with the kernel flipped
-// and the channel roles swapped (cin' = cout, cout' = cin).
+// and the channel roles swapped (cin' = cout, cout' = cin); packed straight from the forward weight
+// (RepackJob kind 3)
 static ConvW pack_dgrad_conv(Packer& P, const std::string& wname, int cin, int cout) {
   ConvW c;
   c.cin = cout;
@@ -146,18 +137,12 @@ static ConvW pack_dgrad_conv(Packer& P, const std::string& wname, int cin, int c
   c.kpad = rup(9 * cout, 64);
   c.npad = rup(cin, 128);
   c.B = P.alloc((size_t)c.npad * c.kpad);
-  float* tmp = P.alloc((size_t)cin * cout * 9);
-  const float* src = P.in(wname).first;
-  P.job([=](hipStream_t s) {
-    flip_transpose3x3_kernel<<<ew_blocks((size_t)cin * cout * 9), 256, 0, s>>>(tmp, src, cout, cin);
-    HIPCHK(hipGetLastError());
-  });
-  P.repack(c.B, tmp, 0, 1, c.npad, c.kpad, cin, cout, 3);
+  P.repack(c.B, P.in(wname).first, 3, 1, c.npad, c.kpad, cin, cout, 3);
   P.split_dev(c);
   return c;
 }
 
-// Linear [fout][fin] -> dX = dY W: a Linear with weight W^T [fin][fout].
+// Linear [fout][fin] -> dX = dY W: a Linear with weight W^T [fin][fout] (RepackJob kind 4)
 static ConvW pack_dgrad_linear(Packer& P, const std::string& wname, int fin, int fout) {
   ConvW c;
   c.cin = fout;
@@ -166,10 +151,27 @@ static ConvW pack_dgrad_linear(Packer& P, const std::string& wname, int fin, int
   c.kpad = rup(fout, 64);
   c.npad = rup(fin, 128);
   c.B = P.alloc((size_t)c.npad * c.kpad);
-  float* tmp = P.transposed(wname, fout, fin);
-  P.repack(c.B, tmp, 1, 1, c.npad, c.kpad, fin, fout, 1);
+  P.repack(c.B, P.in(wname).first, 4, 1, c.npad, c.kpad, fin, fout, 1);
   P.split_dev(c);
   return c;
+}
+
+// the recorded device splits (Packer::split_dev) as two batched launches
+static void run_split_jobs(dmx_model* m, hipStream_t st) {
+  const size_t nj = m->split_jobs.size();
+  if (nj == 0) return;
+  if (m->split_table_n != nj) {
+    if (m->split_table) HIPCHK(hipFree(m->split_table));
+    m->split_table = nullptr;
+    HIPCHK(hipMalloc(&m->split_table, nj * sizeof(SplitJob)));
+    HIPCHK(hipMemcpy(m->split_table, m->split_jobs.data(), nj * sizeof(SplitJob), hipMemcpyHostToDevice));
+    m->split_table_n = nj;
+  }
+  const SplitJob* t = static_cast<const SplitJob*>(m->split_table);
+  absmax_batch_kernel<<<dim3(SPLIT_PARTS, (unsigned)nj), 256, 0, st>>>(t);
+  HIPCHK(hipGetLastError());
+  split_batch_kernel<<<dim3(64, (unsigned)nj), 256, 0, st>>>(t);
+  HIPCHK(hipGetLastError());
 }
 
 static void ensure_train(dmx_model* m, hipStream_t st) {
@@ -194,6 +196,7 @@ static void ensure_train(dmx_model* m, hipStream_t st) {
     a.df1 = pack_dgrad_linear(P, a.prefix + ".ff_self.1.weight", c, c);
     a.df2 = pack_dgrad_linear(P, a.prefix + ".ff_self.3.weight", c, c);
   }
+  run_split_jobs(m, st);
   HIPCHK(hipStreamSynchronize(st));
   m->train_ready = true;
 }
@@ -933,7 +936,7 @@ static void refresh_model(dmx_model* m, hipStream_t st) {
     repack_batch_kernel<<<dim3(64, (unsigned)nr), 256, 0, st>>>(rt);
     HIPCHK(hipGetLastError());
   }
-  for (auto& f : m->post_jobs) f(st);  // device-side splits of the data-gradient weights
+  run_split_jobs(m, st);  // device-side splits of the data-gradient weights
   m->planes_stale = true;
 }
 
