@@ -314,6 +314,7 @@ struct dmx_model {
   std::vector<dmx::RepackJob> repacks;  // (one launch each) by dmx_model_refresh
   void* job_tables = nullptr;           // device copies of the two tables
   size_t job_tables_n = 0;              // copies.size() + repacks.size() when uploaded
+  size_t copy_chunks = 0, repack_chunks = 0, repack_tiles = 0;  // BatchChunk / RepackTile entries (kernels.h)
   bool planes_stale = false;
   unsigned* amax = nullptr;  // absmax scratch of split_planes
   // training (train_engine.h): tape of the last dmx_train_forward, its workspace and the
@@ -2090,10 +2091,13 @@ static void vae_enc_body(Run& R, const float* x, const float* eps, float* z, flo
     H = Ho;
     W = Wo;
   }
+  const int nb = cdiv(H * W, 32);
+  float* klp = R.ws.get<float>((size_t)n * nb);
   if (R.plan) return;
   R.begin("vae_enc_tail_kernel", 2.0 * n * H * W * 8 * 256, 4.0 * (double)n * H * W * (256 + 4 + 4));
-  vae_enc_tail_kernel<<<n, 256, 0, R.st>>>(act, m->wmu, m->bmu, m->wlv, m->blv, eps, z, kl, H * W, m->cfg.scale,
-                                            1.0f / ((float)h * (float)w), m->range_flag);
+  vae_enc_tail_kernel<<<dim3(nb, n), 256, 0, R.st>>>(act, m->wmu, m->bmu, m->wlv, m->blv, eps, z, klp, H * W,
+                                                      m->cfg.scale, m->range_flag);
+  vae_enc_kl_kernel<<<cdiv(n, 64), 64, 0, R.st>>>(klp, nb, n, 1.0f / ((float)h * (float)w), kl);
   R.end();
   HIPCHK(hipGetLastError());
 }

@@ -984,50 +984,67 @@ static __global__ __launch_bounds__(256) void vae_tail_kernel(const float* in, c
 // VAE encoder tail (models/vae.py:52-60): to_mu / to_logvar (1x1 convs 256 -> 4, bias),
 // logvar.clamp(-30, 20), std = exp(0.5 logvar), z = (mu + eps * std) * scale with eps the
 // reference's randn_like draw (passed in, NCHW), and the per-sample KL term
-// 0.5 * sum_{c,y,x}(exp(lv) + mu^2 - 1 - lv) / (H_img * W_img).  One block per sample; the KL
-// sum is reduced in a fixed order (per-thread strided partials, then a fixed tree).
+// 0.5 * sum_{c,y,x}(exp(lv) + mu^2 - 1 - lv) / (H_img * W_img).  Grid (cdiv(HW, 32), N): 32 pixels per
+// block, 8 lanes per pixel (channels 4 lane + 32 i: 128-byte coalesced rows, conflict-free weight
+// reads) reduced by shuffles; the KL terms per block in a fixed order to klp[n][block], summed in
+// block order by vae_enc_kl_kernel.
 // in: materialised GELU(GN(enc.15)) NHWC [N][HW][256].
 static __global__ __launch_bounds__(256) void vae_enc_tail_kernel(const float* in, const float* wmu, const float* bmu,
                                                            const float* wlv, const float* blv, const float* eps,
-                                                           float* z, float* kl, int HW, float scale, float inv_px,
+                                                           float* z, float* klp, int HW, float scale,
                                                            int* range_flag) {
-  __shared__ float ws[8][256];  // rows 0-3: to_mu, 4-7: to_logvar ([out][in] of the 1x1 convs)
-  __shared__ float red[256];
+  __shared__ __attribute__((aligned(16))) float ws[8][256];  // rows 0-3: to_mu, 4-7: to_logvar ([out][in])
+  __shared__ float red[4];
   for (int i = threadIdx.x; i < 8 * 256; i += 256) ws[i / 256][i % 256] = i < 1024 ? wmu[i] : wlv[i - 1024];
   __syncthreads();
-  const int n = blockIdx.x;
+  const int n = blockIdx.y, l8 = threadIdx.x & 7, pix = blockIdx.x * 32 + (threadIdx.x >> 3);
+  float a[8];
+#pragma unroll
+  for (int o = 0; o < 8; ++o) a[o] = 0.f;
+  if (pix < HW) {
+    const float* src = in + ((size_t)n * HW + pix) * 256 + 4 * l8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const floatx4 v = ld4(src + 32 * i);
+#pragma unroll
+      for (int o = 0; o < 8; ++o) {
+        const floatx4 w = *reinterpret_cast<const floatx4*>(&ws[o][32 * i + 4 * l8]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[o] += v[j] * w[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < 8; ++o) {
+    a[o] += __shfl_xor(a[o], 1, 64);
+    a[o] += __shfl_xor(a[o], 2, 64);
+    a[o] += __shfl_xor(a[o], 4, 64);
+  }
   float kacc = 0.f;
-  for (int pix = threadIdx.x; pix < HW; pix += 256) {
-    const float* src = in + ((size_t)n * HW + pix) * 256;
-    float a[8];
+  if (l8 == 0 && pix < HW) {
 #pragma unroll
     for (int o = 0; o < 4; ++o) {
-      a[o] = bmu[o];
-      a[o + 4] = blv[o];
-    }
-    for (int c = 0; c < 256; c += 4) {
-      const floatx4 v = ld4(src + c);
-#pragma unroll
-      for (int o = 0; o < 8; ++o)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) a[o] += v[j] * ws[o][c + j];
-    }
-#pragma unroll
-    for (int o = 0; o < 4; ++o) {
-      flag_nonfinite(range_flag, a[o] + a[o + 4]);
-      const float mu = a[o], lv = fminf(fmaxf(a[o + 4], -30.f), 20.f);
+      const float mu0 = a[o] + bmu[o], lv0 = a[o + 4] + blv[o];
+      flag_nonfinite(range_flag, mu0 + lv0);
+      const float mu = mu0, lv = fminf(fmaxf(lv0, -30.f), 20.f);
       const size_t idx = ((size_t)n * 4 + o) * HW + pix;
       z[idx] = (mu + eps[idx] * expf(0.5f * lv)) * scale;
       kacc += ((expf(lv) + mu * mu) - 1.f) - lv;
     }
   }
-  red[threadIdx.x] = kacc;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) kacc += __shfl_xor(kacc, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = kacc;
   __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-    __syncthreads();
+  if (threadIdx.x == 0) klp[(size_t)n * gridDim.x + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+// kl[n] = 0.5 * (sum of the tail's block partials in block order) / (H_img * W_img)
+static __global__ void vae_enc_kl_kernel(const float* klp, int nb, int N, float inv_px, float* kl) {
+  for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < N; n += gridDim.x * blockDim.x) {
+    float sacc = 0.f;
+    for (int b = 0; b < nb; ++b) sacc += klp[(size_t)n * nb + b];
+    kl[n] = 0.5f * sacc * inv_px;
   }
-  if (threadIdx.x == 0) kl[n] = 0.5f * red[0] * inv_px;
 }
 
 // Weight repack into the implicit-GEMM B layout [phase][Npad][Kpad] (zero pad).
@@ -1048,8 +1065,8 @@ struct CopyJob {
 };
 
 DMX_DEV void repack_range(float* dst, const float* src, int kind, int P, int Npad, int Kpad, int Cout, int Cin, int KS,
-                          unsigned first, unsigned stride) {
-  const unsigned total = (unsigned)P * (unsigned)Npad * (unsigned)Kpad, kp = (unsigned)Kpad, np = (unsigned)Npad;
+                          unsigned first, unsigned stride, unsigned end = ~0u) {
+  const unsigned total = min((unsigned)P * (unsigned)Npad * (unsigned)Kpad, end), kp = (unsigned)Kpad, np = (unsigned)Npad;
   for (unsigned i = first; i < total; i += stride) {
     const unsigned row = i / kp;
     const int k = (int)(i - row * kp), nn = (int)(row % np), ph = (int)(row / np);
@@ -1086,17 +1103,57 @@ static __global__ void repack_kernel(float* dst, const float* src, int kind, int
                gridDim.x * blockDim.x);
 }
 
-// dmx_model_refresh: every weight repack (blockIdx.y = job) / parameter copy of the model in one
-// launch each instead of one launch per tensor (the refresh follows every optimizer step).
-static __global__ void repack_batch_kernel(const RepackJob* jobs) {
-  const RepackJob j = jobs[blockIdx.y];
-  repack_range(j.dst, j.src, j.kind, j.P, j.Npad, j.Kpad, j.Cout, j.Cin, j.KS, blockIdx.x * blockDim.x + threadIdx.x,
-               gridDim.x * blockDim.x);
+// dmx_model_refresh: every weight repack / parameter copy of the model in one launch each instead of
+// one launch per tensor (the refresh follows every optimizer step).  The jobs are cut into chunks of
+// BATCH_CHUNK elements (one block each, table built on the host), so a launch's blocks carry equal
+// work whatever the tensor sizes.
+constexpr unsigned BATCH_CHUNK = 8192;
+struct BatchChunk {
+  unsigned job, first;
+};
+static __global__ __launch_bounds__(256) void repack_batch_kernel(const RepackJob* jobs, const BatchChunk* chunks) {
+  const BatchChunk c = chunks[blockIdx.x];
+  const RepackJob j = jobs[c.job];
+  repack_range(j.dst, j.src, j.kind, j.P, j.Npad, j.Kpad, j.Cout, j.Cin, j.KS, c.first + threadIdx.x, 256,
+               c.first + BATCH_CHUNK);
 }
-static __global__ void copy_batch_kernel(const CopyJob* jobs) {
-  const CopyJob j = jobs[blockIdx.y];
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < j.n; i += (size_t)gridDim.x * blockDim.x)
-    j.dst[i] = j.src[i];
+// The 3x3 conv repacks (kind 0: B[n][t Cin + c] = src[n][c][t]; kind 3: B[n][t Cin + c] =
+// src[c][n][8 - t]) as LDS-tiled transposes: a block takes 16 rows n x 32 channels c (x 9 taps), reads
+// the source in its contiguous runs (288 / 144 floats) and writes 128-byte runs of B.  Only the live
+// region (n < Cout, k < 9 Cin) is rewritten: the zero padding of B never changes after the first pack.
+struct RepackTile {
+  unsigned job, n0, c0;
+};
+static __global__ __launch_bounds__(256) void repack_tile_kernel(const RepackJob* jobs, const RepackTile* tiles) {
+  __shared__ float T[32 * 145];
+  const RepackTile tl = tiles[blockIdx.x];
+  const RepackJob j = jobs[tl.job];
+  const int n0 = (int)tl.n0, c0 = (int)tl.c0, nr = min(16, j.Cout - n0), nc = min(32, j.Cin - c0);
+  if (j.kind == 0) {  // src rows n: [Cin][9] contiguous; T[r][cl][t] at r * 288 + cl * 9 + t
+    for (int e = threadIdx.x; e < 16 * 288; e += 256) {
+      const int r = e / 288, q = e - r * 288;
+      if (r < nr && q < nc * 9) T[e] = j.src[((size_t)(n0 + r) * j.Cin + c0) * 9 + q];
+    }
+  } else {  // src [Cin][Cout][9]: per channel c, rows n0 .. n0 + 15 contiguous; T[cl][r][t] at cl * 145 + r * 9 + t
+    for (int e = threadIdx.x; e < 32 * 144; e += 256) {
+      const int cl = e / 144, q = e - cl * 144;
+      if (cl < nc && q < nr * 9) T[cl * 145 + q] = j.src[((size_t)(c0 + cl) * j.Cout + n0) * 9 + q];
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 16 * 9 * 32; e += 256) {
+    const int cl = e & 31, t = (e >> 5) % 9, r = e / 288;
+    if (r < nr && cl < nc) {
+      const float v = j.kind == 0 ? T[r * 288 + cl * 9 + t] : T[cl * 145 + r * 9 + (8 - t)];
+      j.dst[(size_t)(n0 + r) * j.Kpad + t * j.Cin + c0 + cl] = v;
+    }
+  }
+}
+static __global__ __launch_bounds__(256) void copy_batch_kernel(const CopyJob* jobs, const BatchChunk* chunks) {
+  const BatchChunk c = chunks[blockIdx.x];
+  const CopyJob j = jobs[c.job];
+  const size_t end = min(j.n, (size_t)c.first + BATCH_CHUNK);
+  for (size_t i = (size_t)c.first + threadIdx.x; i < end; i += 256) j.dst[i] = j.src[i];
 }
 
 // Transpose [R][Cc] -> [Cc][R] (embedding weights for coalesced access).

@@ -917,23 +917,54 @@ static void refresh_model(dmx_model* m, hipStream_t st) {
   if (!m->finalized) throw Error(DMX_E_STATE, "model weights not finalized");
   const size_t nc = m->copies.size(), nr = m->repacks.size();
   if (m->job_tables_n != nc + nr) {  // (re)upload the tables (training adds repacks after finalize)
+    std::vector<BatchChunk> cc, rc;
+    for (size_t i = 0; i < nc; ++i)
+      for (size_t f = 0; f < m->copies[i].n; f += BATCH_CHUNK) cc.push_back(BatchChunk{(unsigned)i, (unsigned)f});
+    std::vector<RepackTile> tc;
+    for (size_t i = 0; i < nr; ++i) {
+      const RepackJob& r = m->repacks[i];
+      const size_t total = (size_t)r.P * r.Npad * r.Kpad;
+      if (total >= (1ull << 32)) throw Error(DMX_E_INTERNAL, "refresh: weight too large for 32-bit repack");
+      if ((r.kind == 0 || r.kind == 3) && r.KS == 3 && r.P == 1) {  // LDS-tiled (live region only)
+        for (int n0 = 0; n0 < r.Cout; n0 += 16)
+          for (int c0 = 0; c0 < r.Cin; c0 += 32) tc.push_back(RepackTile{(unsigned)i, (unsigned)n0, (unsigned)c0});
+        continue;
+      }
+      for (size_t f = 0; f < total; f += BATCH_CHUNK) rc.push_back(BatchChunk{(unsigned)i, (unsigned)f});
+    }
     if (m->job_tables) HIPCHK(hipFree(m->job_tables));
     m->job_tables = nullptr;
-    HIPCHK(hipMalloc(&m->job_tables, nc * sizeof(CopyJob) + nr * sizeof(RepackJob) + 16));
-    HIPCHK(hipMemcpy(m->job_tables, m->copies.data(), nc * sizeof(CopyJob), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(static_cast<char*>(m->job_tables) + nc * sizeof(CopyJob), m->repacks.data(),
-                     nr * sizeof(RepackJob), hipMemcpyHostToDevice));
+    const size_t b0 = nc * sizeof(CopyJob), b1 = nr * sizeof(RepackJob), b2 = cc.size() * sizeof(BatchChunk),
+                 b3 = rc.size() * sizeof(BatchChunk), b4 = tc.size() * sizeof(RepackTile);
+    HIPCHK(hipMalloc(&m->job_tables, b0 + b1 + b2 + b3 + b4 + 16));
+    char* t = static_cast<char*>(m->job_tables);
+    HIPCHK(hipMemcpy(t, m->copies.data(), b0, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(t + b0, m->repacks.data(), b1, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(t + b0 + b1, cc.data(), b2, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(t + b0 + b1 + b2, rc.data(), b3, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(t + b0 + b1 + b2 + b3, tc.data(), b4, hipMemcpyHostToDevice));
     m->job_tables_n = nc + nr;
+    m->copy_chunks = cc.size();
+    m->repack_chunks = rc.size();
+    m->repack_tiles = tc.size();
   }
-  const CopyJob* ct = static_cast<const CopyJob*>(m->job_tables);
-  const RepackJob* rt = reinterpret_cast<const RepackJob*>(static_cast<const char*>(m->job_tables) + nc * sizeof(CopyJob));
-  if (nc) {
-    copy_batch_kernel<<<dim3(4, (unsigned)nc), 256, 0, st>>>(ct);
+  const char* t = static_cast<const char*>(m->job_tables);
+  const CopyJob* ct = reinterpret_cast<const CopyJob*>(t);
+  const RepackJob* rt = reinterpret_cast<const RepackJob*>(t + nc * sizeof(CopyJob));
+  const BatchChunk* cch = reinterpret_cast<const BatchChunk*>(t + nc * sizeof(CopyJob) + nr * sizeof(RepackJob));
+  const BatchChunk* rch = cch + m->copy_chunks;
+  const RepackTile* rtl = reinterpret_cast<const RepackTile*>(rch + m->repack_chunks);
+  if (m->copy_chunks) {
+    copy_batch_kernel<<<(unsigned)m->copy_chunks, 256, 0, st>>>(ct, cch);
     HIPCHK(hipGetLastError());
   }
   for (auto& f : m->jobs) f(st);
-  if (nr) {
-    repack_batch_kernel<<<dim3(64, (unsigned)nr), 256, 0, st>>>(rt);
+  if (m->repack_chunks) {
+    repack_batch_kernel<<<(unsigned)m->repack_chunks, 256, 0, st>>>(rt, rch);
+    HIPCHK(hipGetLastError());
+  }
+  if (m->repack_tiles) {
+    repack_tile_kernel<<<(unsigned)m->repack_tiles, 256, 0, st>>>(rt, rtl);
     HIPCHK(hipGetLastError());
   }
   run_split_jobs(m, st);  // device-side splits of the data-gradient weights
