@@ -384,33 +384,40 @@ static __global__ __launch_bounds__(256) void wgrad_kernel(const WgradParams p) 
   }
 }
 
-// Weight gradient on the f16 matrix cores (x3 split, fp32 accumulate): the tiling of round 5's fp32
-// kernel (64 Cout x 128 K per block, 2 x 2 waves of 32 x 64, 32-row stages, double-buffered), with the staged
-// rows split once into f16 hi / lo planes kept row-major in LDS ([m][co], [m][k]) and the MFMA operands
-// — contraction over m, 8 consecutive rows per lane — read with ds_read_b64_tr_b16: per 16-lane group a
-// 4-row x 16-column block, lane 4q + p addressing row q, columns 4p .. 4p + 3, lane i receiving column i
-// (MI355X guide T10).  dY is multiplied by 2^ea (its max |dY| 2^ea in [2^12, 2^13): the lo parts stay
-// f16-normal) and the slabs by 2^-ea.  Row pitches of 96 / 160 halves (48 / 80 banks: the 4 rows of a
-// block on 4 disjoint 16-bank ranges) make the transposed reads conflict-free.  The bias gradient
-// (column sums of dY) is summed from the staged registers: lanes, then the 4 waves in a fixed order.
+// Weight gradient on the f16 matrix cores (x3 split, fp32 accumulate): block tile CO (64 or 128) Cout x
+// 128 K, 2 x 2 waves of CO/2 x 64, 32-row stages, double-buffered, with the staged rows split once into
+// f16 hi / lo planes kept row-major in LDS ([m][co], [m][k]) and the MFMA operands — contraction over m,
+// 8 consecutive rows per lane — read with ds_read_b64_tr_b16: per 16-lane group a 4-row x 16-column
+// block, lane 4q + p addressing row q, columns 4p .. 4p + 3, lane i receiving column i (MI355X guide
+// T10).  dY is multiplied by 2^ea (its max |dY| 2^ea in [2^12, 2^13): the lo parts stay f16-normal) and
+// the slabs by 2^-ea.  Row pitches of CO + 32 / 160 halves (48 or 80 banks: the 4 rows of a block on 4
+// disjoint 16-bank ranges) make the transposed reads conflict-free.  CO = 128 (Cout % 128 == 0) stages
+// each X row once for twice the MFMA work of CO = 64 (the split and im2col VALU per product halve).
+// The bias gradient (column sums of dY) is summed from the staged registers: lanes, then the 4 waves
+// in a fixed order.
 constexpr int WG_BM = 32;  // rows per stage
 typedef __fp16 fp16x4_t __attribute__((__vector_size__(4 * sizeof(__fp16))));
 DMX_DEV half4 lds_tr16(const _Float16* p) {
   return __builtin_bit_cast(half4, __builtin_amdgcn_ds_read_tr16_b64_v4f16(
                                        (__attribute__((address_space(3))) fp16x4_t*)(p)));
 }
+template <int CO>
 static __global__ __launch_bounds__(256) void wgrad_x3_kernel(const WgradParams p) {
-  constexpr int DP = 96, XP = 160;  // plane row pitches (halves)
+  constexpr int DP = CO + 32, XP = 160;  // plane row pitches (halves)
+  constexpr int MT = CO / 64;            // 32-row m-tiles per wave
+  constexpr int DL = CO / 4;             // lanes per dY row (one float4 each)
+  constexpr int DR = 256 / DL;           // dY rows per pass
+  constexpr int DI = WG_BM / DR;         // dY float4 per thread per stage
   __shared__ __attribute__((aligned(16))) _Float16 Dh[2][WG_BM][DP];
   __shared__ __attribute__((aligned(16))) _Float16 Dl[2][WG_BM][DP];
   __shared__ __attribute__((aligned(16))) _Float16 Xh[2][WG_BM][XP];
   __shared__ __attribute__((aligned(16))) _Float16 Xl[2][WG_BM][XP];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, wm = wv >> 1, wn = wv & 1;
-  const int co0 = blockIdx.x * 64, k0 = blockIdx.y * 128;
+  const int co0 = blockIdx.x * CO, k0 = blockIdx.y * 128;
   const int mbeg = blockIdx.z * p.rows_per_split, mend = min(p.M, mbeg + p.rows_per_split);
   const int HW = p.H * p.W;
   const float rhw = 1.f / (float)HW, rw = 1.f / (float)p.W;
-  const int dr = tid >> 4, dc = (tid & 15) * 4;  // dY: rows dr + 16 i (i < 2), float4 dc
+  const int dr = tid / DL, dc = (tid % DL) * 4;  // dY: rows dr + DR i (i < DI), float4 dc
   const int xr = tid >> 5, xc = (tid & 31) * 4;  // X: rows xr + 8 i (i < 4), float4 xc
   const int k = k0 + xc;
   const bool kvalid = k < p.K;
@@ -424,13 +431,13 @@ static __global__ __launch_bounds__(256) void wgrad_x3_kernel(const WgradParams 
   const float a_sc = ldexpf(1.f, ea), o_sc = ldexpf(1.f, -ea);
   const bool bias = p.bpart != nullptr && blockIdx.y == 0;
   floatx4 bs = {0.f, 0.f, 0.f, 0.f};  // column sums of dY (columns dc .. dc + 3) over this thread's rows
-  floatx4 rdv[2][2], rxv[2][4];  // two register stages (the loads run two 32-row stages ahead)
+  floatx4 rdv[2][DI], rxv[2][4];      // two register stages (the loads run two 32-row stages ahead)
   auto load = [&](int m0, int rs) {
-    floatx4(&rd)[2] = rdv[rs];
+    floatx4(&rd)[DI] = rdv[rs];
     floatx4(&rx)[4] = rxv[rs];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int m = m0 + dr + 16 * i;
+    for (int i = 0; i < DI; ++i) {
+      const int m = m0 + dr + DR * i;
       rd[i] = m < mend ? *reinterpret_cast<const floatx4*>(p.dy + (size_t)m * p.Cout + co0 + dc)
                        : floatx4{0.f, 0.f, 0.f, 0.f};
     }
@@ -453,18 +460,18 @@ static __global__ __launch_bounds__(256) void wgrad_x3_kernel(const WgradParams 
     }
   };
   auto store = [&](int b, int rs) {
-    floatx4(&rd)[2] = rdv[rs];
+    floatx4(&rd)[DI] = rdv[rs];
     floatx4(&rx)[4] = rxv[rs];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < DI; ++i) {
       if (bias) bs += rd[i];
       floatx4 v = rd[i];
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] *= a_sc;
       half4 h, l;
       split4(v, h, l);
-      *reinterpret_cast<half4*>(&Dh[b][dr + 16 * i][dc]) = h;
-      *reinterpret_cast<half4*>(&Dl[b][dr + 16 * i][dc]) = l;
+      *reinterpret_cast<half4*>(&Dh[b][dr + DR * i][dc]) = h;
+      *reinterpret_cast<half4*>(&Dl[b][dr + DR * i][dc]) = l;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -474,11 +481,13 @@ static __global__ __launch_bounds__(256) void wgrad_x3_kernel(const WgradParams 
       *reinterpret_cast<half4*>(&Xl[b][xr + 8 * i][xc]) = l;
     }
   };
-  floatx16 acc[2];
+  floatx16 acc[MT][2];
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int t = 0; t < MT; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][j][r] = 0.f;
   // transposed-read addressing: group g = lane / 16 (rows + 8 for g >= 2, columns + 16 for odd g),
   // lane 4q + p of the group -> row q, columns 4p .. 4p + 3
   const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
@@ -488,10 +497,15 @@ static __global__ __launch_bounds__(256) void wgrad_x3_kernel(const WgradParams 
 #pragma unroll
     for (int s = 0; s < WG_BM; s += 16) {
       const int r0 = s + trow;
-      const half4 a0 = lds_tr16(&Dh[b][r0][wm * 32 + tcol]), a1 = lds_tr16(&Dh[b][r0 + 4][wm * 32 + tcol]);
-      const half4 c0 = lds_tr16(&Dl[b][r0][wm * 32 + tcol]), c1 = lds_tr16(&Dl[b][r0 + 4][wm * 32 + tcol]);
-      const half8 ah = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-      const half8 al = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+      half8 ah[MT], al[MT];
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const int cd = wm * (CO / 2) + 32 * t + tcol;
+        const half4 a0 = lds_tr16(&Dh[b][r0][cd]), a1 = lds_tr16(&Dh[b][r0 + 4][cd]);
+        const half4 c0 = lds_tr16(&Dl[b][r0][cd]), c1 = lds_tr16(&Dl[b][r0 + 4][cd]);
+        ah[t] = half8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        al[t] = half8{c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+      }
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
         const int cx = wn * 64 + 32 * n + tcol;
@@ -499,9 +513,12 @@ static __global__ __launch_bounds__(256) void wgrad_x3_kernel(const WgradParams 
         const half4 d0 = lds_tr16(&Xl[b][r0][cx]), d1 = lds_tr16(&Xl[b][r0 + 4][cx]);
         const half8 bh = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
         const half8 bl = {d0[0], d0[1], d0[2], d0[3], d1[0], d1[1], d1[2], d1[3]};
-        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bh, acc[n], 0, 0, 0);
-        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bl, acc[n], 0, 0, 0);
-        acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bh, acc[n], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          acc[t][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[t], bh, acc[t][n], 0, 0, 0);
+          acc[t][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t], bl, acc[t][n], 0, 0, 0);
+          acc[t][n] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[t], bh, acc[t][n], 0, 0, 0);
+        }
       }
     }
   };
@@ -521,26 +538,28 @@ static __global__ __launch_bounds__(256) void wgrad_x3_kernel(const WgradParams 
     body(st, 0);
     if (st + 1 < nst) body(st + 1, 1);
   }
-  if (bias) {  // lanes sharing columns (xor 16, 32), then waves 0..3 in order through LDS
+  if (bias) {  // lanes sharing columns (same tid % DL), then waves 0..3 in order through LDS
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      bs[e] += __shfl_xor(bs[e], 16, 64);
-      bs[e] += __shfl_xor(bs[e], 32, 64);
-    }
+    for (int o = DL; o < 64; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bs[e] += __shfl_xor(bs[e], o, 64);
     float* red = reinterpret_cast<float*>(&Dh[0][0][0]);  // (the stages are done: last barrier above)
-    if (lane < 16) *reinterpret_cast<floatx4*>(&red[wv * 64 + dc]) = bs;
+    if (lane < DL) *reinterpret_cast<floatx4*>(&red[wv * CO + dc]) = bs;
     __syncthreads();
-    if (tid < 64) p.bpart[(size_t)blockIdx.z * p.Cout + co0 + tid] = ((red[tid] + red[64 + tid]) + red[128 + tid]) + red[192 + tid];
+    if (tid < CO)
+      p.bpart[(size_t)blockIdx.z * p.Cout + co0 + tid] = ((red[tid] + red[CO + tid]) + red[2 * CO + tid]) + red[3 * CO + tid];
   }
   float* dst = p.part + (size_t)blockIdx.z * p.Cout * p.K;
 #pragma unroll
-  for (int j = 0; j < 2; ++j)
+  for (int t = 0; t < MT; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int co = co0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      const int kk = k0 + wn * 64 + j * 32 + (lane & 31);
-      if (kk < p.K) dst[(size_t)co * p.K + kk] = acc[j][r] * o_sc;
-    }
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = co0 + wm * (CO / 2) + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int kk = k0 + wn * 64 + j * 32 + (lane & 31);
+        if (kk < p.K) dst[(size_t)co * p.K + kk] = acc[t][j][r] * o_sc;
+      }
 }
 
 // grad (torch layout) = sum over the split slabs; k = tap * Cin + ci -> [co][ci][tap] (input channels

@@ -536,7 +536,8 @@ static void wgrad(Run& R, const float* dy, const float* x, int N, int H, int W, 
                   int cin_real, float* grad, float* bias_grad_out = nullptr) {
   const int M = N * H * W, K = taps * Cin;
   const bool fast = Cin % 64 == 0 && Cout % 64 == 0;
-  const int bxy = cdiv(Cout, 64) * cdiv(K, fast ? 128 : 64);
+  const int co_t = fast && Cout % 128 == 0 ? 128 : 64;  // wgrad_x3_kernel<128>: X staged once per 128 Cout
+  const int bxy = cdiv(Cout, co_t) * cdiv(K, fast ? 128 : 64);
   // (the x3 kernel runs two 64 KB-LDS blocks per CU: one round of 512 blocks; fewer slabs for
   // wgrad_finish_kernel to read than the fp32 kernel's 1024-block target)
   int splits = std::max(1, std::min(cdiv(fast ? 512 : 1024, bxy), cdiv(M, 256)));
@@ -552,7 +553,8 @@ static void wgrad(Run& R, const float* dy, const float* x, int N, int H, int W, 
     check_range(R, x, (size_t)M * Cin * 4, "wgrad X");
     WgradParams p{dy, x, N, H, W, Cin, Cout, taps, M, K, rps, part, bpart, amax, nparts};
     R.begin("wgrad_kernel", 2.0 * M * (double)Cout * K, 4.0 * ((double)M * (Cout + Cin) + (double)splits * Cout * K));
-    if (fast) wgrad_x3_kernel<<<dim3(Cout / 64, cdiv(K, 128), splits), 256, 0, R.st>>>(p);
+    if (fast && co_t == 128) wgrad_x3_kernel<128><<<dim3(Cout / 128, cdiv(K, 128), splits), 256, 0, R.st>>>(p);
+    else if (fast) wgrad_x3_kernel<64><<<dim3(Cout / 64, cdiv(K, 128), splits), 256, 0, R.st>>>(p);
     else wgrad_kernel<<<dim3(cdiv(Cout, 64), cdiv(K, 64), splits), 256, 0, R.st>>>(p);
     R.end();
     HIPCHK(hipGetLastError());
