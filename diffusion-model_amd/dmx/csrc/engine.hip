@@ -790,6 +790,7 @@ struct Run {
   size_t amax_n = 0;
   unsigned* amax_slot = nullptr;
   int amax_parts = 0;
+  int amax_uses = 0;  // remaining reuses of that measurement
   void tap(const std::string& name, const float* p, size_t count);
   std::string ck_layer;
   // DMX_CKSUM: one workspace checksum per layer, taken when the next layer's first kernel begins

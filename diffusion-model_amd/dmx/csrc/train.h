@@ -44,6 +44,8 @@ struct GnBwdParams {
   int chunks, ppb;       // pass A: blocks per sample, pixels per block
   double* bsum;          // [N][chunks][2] block partials of S1, S2
   float* bch;            // [N][chunks][3][C] block partials of dgamma, dbeta, demb
+  unsigned* amax_part;   // or null: per-block max |dr| ([N][gridDim.x], absmax_part_kernel's format) — the
+                         // device-side operand scale of the x3 weight / data gradients that read dr
 };
 
 DMX_DEV float2 gn_stats_from_rowpart(const GnBwdParams& p, int n, double* red) {
@@ -208,15 +210,27 @@ static __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const GnBwdPar
   const float m1 = s12[0] / cnt, m2 = s12[1] / cnt;
   const size_t base = (size_t)n * p.HW * p.C;
   const int per = p.HW * p.C;
+  float mx = 0.f;
   for (int i = blockIdx.x * 256 + tid; i < per; i += gridDim.x * 256) {
     const int c = i % p.C;
     const size_t idx = base + i;
     const float xh = (p.r[idx] - st.x) * st.y;
     float dres;
     const float dy = gn_dy(p, idx, c, xh, dres);
-    p.dr[idx] = st.y * (p.gamma[c] * dy - m1 - xh * m2);
+    const float d = st.y * (p.gamma[c] * dy - m1 - xh * m2);
+    p.dr[idx] = d;
+    mx = fmaxf(mx, fabsf(d));
     if (p.dres_mode == 1) p.dres[idx] = dres;
     else if (p.dres_mode == 2) p.dres[idx] += dres;
+  }
+  if (p.amax_part != nullptr) {
+    __shared__ float wm[4];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    if ((tid & 63) == 0) wm[tid >> 6] = mx;
+    __syncthreads();
+    if (tid == 0)
+      p.amax_part[(size_t)n * gridDim.x + blockIdx.x] = __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3])));
   }
 }
 

@@ -510,8 +510,8 @@ static void bias_grad(Run& R, const float* dy, int M, int C, float* out) { colsu
 // on the same tensor, and then dropped — a later call on that buffer (its content may have changed)
 // measures again.  Same decisions in the plan and the real pass (arena pointers correspond one to one).
 static const unsigned* dy_amax(Run& R, const float* dy, size_t n, int* parts) {
-  if (R.amax_src == dy && R.amax_n == n) {
-    R.amax_src = nullptr;  // (single use)
+  if (R.amax_src == dy && R.amax_n == n && R.amax_uses > 0) {
+    if (--R.amax_uses == 0) R.amax_src = nullptr;
     *parts = R.amax_parts;
     return R.amax_slot;
   }
@@ -527,15 +527,18 @@ static const unsigned* dy_amax(Run& R, const float* dy, size_t n, int* parts) {
   R.amax_n = n;
   R.amax_slot = slot;
   R.amax_parts = np;
+  R.amax_uses = 1;
   *parts = np;
   return slot;
 }
+
+static bool wgrad_fast(int Cin, int Cout) { return Cin % 64 == 0 && Cout % 64 == 0; }
 
 // weight gradient of a conv3x3 (taps 9) / Linear (taps 1) over NHWC input x and NHWC dY
 static void wgrad(Run& R, const float* dy, const float* x, int N, int H, int W, int Cin, int Cout, int taps,
                   int cin_real, float* grad, float* bias_grad_out = nullptr) {
   const int M = N * H * W, K = taps * Cin;
-  const bool fast = Cin % 64 == 0 && Cout % 64 == 0;
+  const bool fast = wgrad_fast(Cin, Cout);
   const int co_t = fast && Cout % 128 == 0 ? 128 : 64;  // wgrad_x3_kernel<128>: X staged once per 128 Cout
   const int bxy = cdiv(Cout, co_t) * cdiv(K, fast ? 128 : 64);
   // (the x3 kernel runs two 64 KB-LDS blocks per CU: one round of 512 blocks; fewer slabs for
@@ -593,26 +596,39 @@ static void dgrad(Run& R, const float* dy, int Cy, int N, int H, int W, const Co
 static void gn_bwd_launch(Run& R, const float* r, const float2* rp, int nseg, int rrows, const Vec& g, const Vec& b,
                           const float* res, int act, const float* dout, int N, int C, int HW, float* dr, float* dres,
                           int dres_mode, float* chpart, float* demb, int demb_stride, int demb_off,
-                          int ppb, double* bsum, float* bch);
+                          int ppb, double* bsum, float* bch, unsigned* amax, int achunks);
+static int gn_bwd_achunks(int HW, int C) { return std::max(1, std::min(64, cdiv(HW * C, 4096))); }
 
 static void gn_bwd(Run& R, const float* r, const float2* rp, int nseg, int rrows, const Vec& g, const Vec& b,
                    const float* res, int act, const float* dout, int N, int C, int HW, float* dr, float* dres,
-                   int dres_mode, float* ggamma, float* gbeta, float* demb, int demb_stride, int demb_off) {
+                   int dres_mode, float* ggamma, float* gbeta, float* demb, int demb_stride, int demb_off,
+                   int amax_uses = 0) {
   // pass A over ~512 blocks in total (>= 16 pixels each)
   const int chunks = std::max(1, std::min(cdiv(512, N), cdiv(HW, 16)));
   const int ppb = cdiv(HW, chunks);
   float* chpart = R.ws.get<float>((size_t)N * 2 * C);
   double* bsum = R.ws.get<double>((size_t)N * chunks * 2);
   float* bch = R.ws.get<float>((size_t)N * chunks * 3 * C);
+  // amax_uses > 0: pass B also writes the per-block max |dr| — the next amax_uses x3 gradient GEMMs
+  // reading dr take their device-side scale from it (dy_amax) instead of a separate absmax pass
+  const int achunks = gn_bwd_achunks(HW, C);
+  unsigned* amax = amax_uses > 0 ? R.ws.get<unsigned>((size_t)N * achunks) : nullptr;
   if (!R.plan) gn_bwd_launch(R, r, rp, nseg, rrows, g, b, res, act, dout, N, C, HW, dr, dres, dres_mode, chpart,
-                             demb, demb_stride, demb_off, ppb, bsum, bch);
+                             demb, demb_stride, demb_off, ppb, bsum, bch, amax, achunks);
+  if (amax_uses > 0) {
+    R.amax_src = dr;
+    R.amax_n = (size_t)N * HW * C;
+    R.amax_slot = amax;
+    R.amax_parts = N * achunks;
+    R.amax_uses = amax_uses;
+  }
   colsum_pair(R, chpart, N, C, 2 * (size_t)C, ggamma, gbeta);
 }
 
 static void gn_bwd_launch(Run& R, const float* r, const float2* rp, int nseg, int rrows, const Vec& g, const Vec& b,
                           const float* res, int act, const float* dout, int N, int C, int HW, float* dr, float* dres,
                           int dres_mode, float* chpart, float* demb, int demb_stride, int demb_off,
-                          int ppb, double* bsum, float* bch) {
+                          int ppb, double* bsum, float* bch, unsigned* amax, int achunks) {
   GnBwdParams p;
   std::memset(&p, 0, sizeof(p));
   p.r = r;
@@ -641,7 +657,7 @@ static void gn_bwd_launch(Run& R, const float* r, const float2* rp, int nseg, in
   gn_bwd_reduce_kernel<<<dim3(p.chunks, N), 256, 0, R.st>>>(p);
   R.end();
   HIPCHK(hipGetLastError());
-  const int achunks = std::max(1, std::min(64, cdiv(HW * C, 4096)));
+  p.amax_part = amax;
   R.begin("gn_bwd_apply_kernel", 0.0, 4.0 * (double)N * HW * C * (res ? 4 : 3));
   gn_bwd_apply_kernel<<<dim3(achunks, N), 256, 0, R.st>>>(p);
   R.end();
@@ -706,13 +722,15 @@ static void res_bwd(Run& R, const TRes& t, const GradMap& G, const float* dout, 
   float* dr2 = R.ws.get<float>((size_t)M * w.cout);
   gn_bwd(R, t.r2, t.rp2, w.cout / seg, t.rr2, w.g2, w.b2, t.residual ? t.x : nullptr, 0, dout, N, w.cout, HW, dr2,
          t.residual ? dx : nullptr, t.residual ? (dx_acc ? 2 : 1) : 0, G(p + ".double_conv.4.weight"),
-         G(p + ".double_conv.4.bias"), t.emb_off >= 0 ? demb : nullptr, demb_stride, t.emb_off);
+         G(p + ".double_conv.4.bias"), t.emb_off >= 0 ? demb : nullptr, demb_stride, t.emb_off,
+         (wgrad_fast(w.mid, w.cout) ? 1 : 0) + 1);
   wgrad(R, dr2, t.a1, N, H, W, w.mid, w.cout, 9, w.mid, G(p + ".double_conv.3.weight"));
   float* da1 = R.ws.get<float>((size_t)M * w.mid);
   dgrad(R, dr2, w.cout, N, H, W, w.d2, da1, false);
   float* dr1 = R.ws.get<float>((size_t)M * w.mid);
   gn_bwd(R, t.r1, t.rp1, w.mid / seg, t.rr1, w.g1, w.b1, nullptr, 1, da1, N, w.mid, HW, dr1, nullptr, 0,
-         G(p + ".double_conv.1.weight"), G(p + ".double_conv.1.bias"), nullptr, 0, 0);
+         G(p + ".double_conv.1.weight"), G(p + ".double_conv.1.bias"), nullptr, 0, 0,
+         (wgrad_fast(w.cin, w.mid) ? 1 : 0) + (dx != nullptr ? 1 : 0));
   wgrad(R, dr1, t.x, N, H, W, w.cin, w.mid, 9, w.cin_real, G(p + ".double_conv.0.weight"));
   if (dx != nullptr) dgrad(R, dr1, w.mid, N, H, W, w.d1, dx, t.residual || dx_acc);
 }
