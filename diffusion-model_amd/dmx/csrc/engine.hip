@@ -200,6 +200,7 @@ struct ResW {
   int cin_real = 0;     // channels of the reference tensor (cin is padded to a multiple of 4)
   std::string prefix;   // state_dict prefix ("down1.maxpool_conv.1")
   ConvW d1, d2;         // training: data-gradient GEMMs (flipped, transposed kernels; train.h)
+  ConvW t1, t2;         // training forward: c1 / c2 with device-split f16 planes (or no planes: fp32)
 };
 struct AttnW {
   ConvW qkv, o, f1, f2;
@@ -207,6 +208,7 @@ struct AttnW {
   int c = 0;
   std::string prefix;
   ConvW dqkv, dout, df1, df2;  // training: transposed Linear weights (data gradients)
+  ConvW tqkv, to, tf1, tf2;    // training forward: device-split planes of qkv / o / f1 / f2
 };
 struct DownUpW {
   ResW r0, r1;
@@ -783,6 +785,7 @@ struct Run {
   int tile_n = 0;
   // non-null: the next gemm() runs the split-precision implicit GEMM with A scaled on the device by
   // this max|A| slot (training data gradients, train_engine.h dgrad)
+  bool fwd_x3 = false;  // training forward: weights with device-split planes (ConvW::inv_dev) run the split GEMM
   const unsigned* a_amax = nullptr;
   int a_nparts = 0;  // a_amax: that many per-block partial maxima (absmax_part_kernel)
   // train_engine.h dy_amax: the last tensor whose |max| partials were taken
@@ -1099,9 +1102,11 @@ static int gemm(Run& R, const SrcDesc& s, int src_mode, int N, int H, int W, con
   const int tiles128 = cdiv(Md, 128) * cdiv(cw.cout, bn) * cw.phases;
   const int bm = tiles128 >= 256 ? 128 : 64;  // 128-row tiles (split K if the grid is then small) from 256 tiles
   const int blocks = cdiv(Md, bm) * cdiv(cw.cout, bn) * cw.phases;
-  // (R.a_amax: a training data gradient on the split GEMM with device-side operand scales — whatever
-  // the model's precision mode, only the implicit-GEMM kernels below carry those scales)
-  const bool x3 = (R.m->prec >= 1 || R.a_amax != nullptr) && src_mode == SRC_PLAIN && cw.Bh != nullptr;
+  // (R.a_amax: a training data gradient on the split GEMM with device-side operand scales; R.fwd_x3:
+  // the training forward's weights with device-split planes — whatever the model's precision mode,
+  // only the implicit-GEMM kernels below carry those scales)
+  const bool x3 = (R.m->prec >= 1 || R.a_amax != nullptr || (R.fwd_x3 && cw.inv_dev != nullptr)) &&
+                  src_mode == SRC_PLAIN && cw.Bh != nullptr;
   if (R.a_amax != nullptr && (!x3 || ash != nullptr || epi == EPI_STATS || gn != nullptr || R.m->prec == 2))
     throw Error(DMX_E_INTERNAL, "gemm: device-scaled operands only on the plain split implicit GEMM");
   const bool x1 = x3 && R.m->prec == 2;  // config-4 fp16: one MFMA on the hi planes

@@ -174,12 +174,28 @@ static void run_split_jobs(dmx_model* m, hipStream_t st) {
   HIPCHK(hipGetLastError());
 }
 
+// The training forward's copy of a forward weight: the same packed fp32 B (refreshed with the model),
+// its own f16 hi / lo planes split on the device with a device-side scale after every refresh (the
+// inference planes keep their host-derived scale and are re-derived lazily), so the forward GEMMs run
+// on the x3 split implicit GEMM; a weight the x3 kernel cannot take (Cin < 64: the padded input
+// conv) keeps no planes and runs the exact-fp32 GEMM.
+static ConvW fwd_x3_weight(Packer& P, const ConvW& c) {
+  ConvW t = c;
+  t.Bh = t.Bl = t.Fh = t.Fl = t.Uh = t.Ul = nullptr;
+  t.inv_dev = nullptr;
+  t.amax_dev = nullptr;
+  if (c.cin >= 64 && c.phases == 1) P.split_dev(t);
+  return t;
+}
+
 static void ensure_train(dmx_model* m, hipStream_t st) {
   if (m->train_ready) return;
   Packer P{m, st};
   auto res = [&](ResW& r, bool need_dx) {
     if (need_dx) r.d1 = pack_dgrad_conv(P, r.prefix + ".double_conv.0.weight", r.cin, r.mid);
     r.d2 = pack_dgrad_conv(P, r.prefix + ".double_conv.3.weight", r.mid, r.cout);
+    r.t1 = fwd_x3_weight(P, r.c1);
+    r.t2 = fwd_x3_weight(P, r.c2);
   };
   res(m->inc, false);  // the network input takes no gradient
   for (int i = 0; i < 3; ++i) {
@@ -195,6 +211,10 @@ static void ensure_train(dmx_model* m, hipStream_t st) {
     a.dout = pack_dgrad_linear(P, a.prefix + ".mha.out_proj.weight", c, c);
     a.df1 = pack_dgrad_linear(P, a.prefix + ".ff_self.1.weight", c, c);
     a.df2 = pack_dgrad_linear(P, a.prefix + ".ff_self.3.weight", c, c);
+    a.tqkv = fwd_x3_weight(P, a.qkv);
+    a.to = fwd_x3_weight(P, a.o);
+    a.tf1 = fwd_x3_weight(P, a.f1);
+    a.tf2 = fwd_x3_weight(P, a.f2);
   }
   run_split_jobs(m, st);
   HIPCHK(hipStreamSynchronize(st));
@@ -244,11 +264,11 @@ static TRes train_res(Run& R, const ResW& w, const float* x, int N, int H, int W
   t.r2 = R.ws.get<float>((size_t)M * w.cout);
   t.rp2 = R.ws.get<float2>((size_t)M * (w.cout / seg));
   t.out = R.ws.get<float>((size_t)M * w.cout);
-  t.rr1 = gemm(R, plain_src(x, w.cin), SRC_PLAIN, N, H, W, w.c1, EPI_STATS, t.r1, nullptr, t.rp1, seg);
+  t.rr1 = gemm(R, plain_src(x, w.cin), SRC_PLAIN, N, H, W, w.t1, EPI_STATS, t.r1, nullptr, t.rp1, seg);
   NormParams n1 = norm_params(t.r1, t.rp1, w.mid / seg, t.rr1, w.g1.p, w.b1.p, w.mid, HW, t.a1);
   n1.act = 1;
   norm(R, n1, N);
-  t.rr2 = gemm(R, plain_src(t.a1, w.mid), SRC_PLAIN, N, H, W, w.c2, EPI_STATS, t.r2, nullptr, t.rp2, seg);
+  t.rr2 = gemm(R, plain_src(t.a1, w.mid), SRC_PLAIN, N, H, W, w.t2, EPI_STATS, t.r2, nullptr, t.rp2, seg);
   NormParams n2 = norm_params(t.r2, t.rp2, w.cout / seg, t.rr2, w.g2.p, w.b2.p, w.cout, HW, t.out);
   if (residual) n2.res = x;
   if (emb != nullptr) {
@@ -279,16 +299,16 @@ static TAttn train_attn(Run& R, const AttnW& a, const float* x, int N, int H, in
   t.out = R.ws.get<float>((size_t)M * C);
   t.st = R.ws.get<float>((size_t)N * 4 * L * 3);
   layernorm(R, x, t.xl, a.l1w, a.l1b, M, C);
-  gemm(R, plain_src(t.xl, C), SRC_PLAIN, N, H, W, a.qkv, EPI_BIAS, t.qkv, nullptr, nullptr, 1);
+  gemm(R, plain_src(t.xl, C), SRC_PLAIN, N, H, W, a.tqkv, EPI_BIAS, t.qkv, nullptr, nullptr, 1);
   attention_core(R, t.qkv, t.ao, N, L, C, t.st);
-  gemm(R, plain_src(t.ao, C), SRC_PLAIN, N, H, W, a.o, EPI_BIAS_RES, t.av, t.xl, nullptr, 1);
+  gemm(R, plain_src(t.ao, C), SRC_PLAIN, N, H, W, a.to, EPI_BIAS_RES, t.av, t.xl, nullptr, 1);
   layernorm(R, t.av, t.al, a.l2w, a.l2b, M, C);
-  gemm(R, plain_src(t.al, C), SRC_PLAIN, N, H, W, a.f1, EPI_BIAS, t.h1, nullptr, nullptr, 1);
+  gemm(R, plain_src(t.al, C), SRC_PLAIN, N, H, W, a.tf1, EPI_BIAS, t.h1, nullptr, nullptr, 1);
   if (!R.plan) {
     gelu_fwd_kernel<<<ew_blocks((size_t)M * C), 256, 0, R.st>>>(t.h1, t.f, (size_t)M * C);
     HIPCHK(hipGetLastError());
   }
-  gemm(R, plain_src(t.f, C), SRC_PLAIN, N, H, W, a.f2, EPI_BIAS_RES, t.out, t.av, nullptr, 1);
+  gemm(R, plain_src(t.f, C), SRC_PLAIN, N, H, W, a.tf2, EPI_BIAS_RES, t.out, t.av, nullptr, 1);
   return t;
 }
 
@@ -316,6 +336,7 @@ static void emb_head_slices(dmx_model* m, int off[6], int hc[6]) {
 
 static void train_fwd_body(Run& R, Tape& T, const TrainArgs& a) {
   dmx_model* m = R.m;
+  R.fwd_x3 = true;  // the ResW::t* / AttnW::t* weights (device-split planes) on the split GEMM
   const int N = a.n, H = a.h, W = a.w, HW = H * W;
   T.n = N;
   T.h = H;
