@@ -311,7 +311,7 @@ struct dmx_model {
   std::vector<std::function<void(hipStream_t)>> jobs;
   std::vector<dmx::SplitJob> split_jobs;  // device-side splits of the training data-gradient weights,
   void* split_table = nullptr;            // replayed batched after the repacks (two launches)
-  size_t split_table_n = 0;
+  size_t split_table_n = 0, split_chunks = 0;
   std::vector<dmx::CopyJob> copies;     // parameter copies and weight repacks, replayed batched
   std::vector<dmx::RepackJob> repacks;  // (one launch each) by dmx_model_refresh
   void* job_tables = nullptr;           // device copies of the two tables

@@ -373,14 +373,18 @@ static __global__ __launch_bounds__(256) void absmax_batch_kernel(const SplitJob
   const SplitJob j = jobs[blockIdx.y];
   absmax_part_body(j.src, j.n, j.amax, blockIdx.x, gridDim.x);
 }
-static __global__ __launch_bounds__(256) void split_batch_kernel(const SplitJob* jobs) {
-  const SplitJob j = jobs[blockIdx.y];
+// blockIdx.x = chunk of SPLIT_CHUNK elements (chunks[] = {job, first}, built on the host)
+constexpr unsigned SPLIT_CHUNK = 8192;
+static __global__ __launch_bounds__(256) void split_batch_kernel(const SplitJob* jobs, const uint2* chunks) {
+  const uint2 c = chunks[blockIdx.x];
+  const SplitJob j = jobs[c.x];
   unsigned mb = 0u;
   for (int i = 0; i < SPLIT_PARTS; ++i) mb = max(mb, j.amax[i]);
   const int e = amax_exp(mb);
   const float scale = ldexpf(1.f, e);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *j.inv = ldexpf(1.f, -e);
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < j.n; i += (size_t)gridDim.x * blockDim.x) {
+  if (c.y == 0 && threadIdx.x == 0) *j.inv = ldexpf(1.f, -e);
+  const size_t end = min(j.n, (size_t)c.y + SPLIT_CHUNK);
+  for (size_t i = (size_t)c.y + threadIdx.x; i < end; i += 256) {
     const float v = j.src[i] * scale;
     const _Float16 h = (_Float16)v;
     j.hi[i] = h;

@@ -156,21 +156,31 @@ static ConvW pack_dgrad_linear(Packer& P, const std::string& wname, int fin, int
   return c;
 }
 
-// the recorded device splits (Packer::split_dev) as two batched launches
+// the recorded device splits (Packer::split_dev) as two batched launches (the split over chunks of
+// SPLIT_CHUNK elements, so every block carries the same work whatever the weight sizes)
 static void run_split_jobs(dmx_model* m, hipStream_t st) {
   const size_t nj = m->split_jobs.size();
   if (nj == 0) return;
   if (m->split_table_n != nj) {
+    std::vector<uint2> ch;
+    for (size_t i = 0; i < nj; ++i) {
+      if (m->split_jobs[i].n >= (1ull << 32)) throw Error(DMX_E_INTERNAL, "split: weight too large");
+      for (size_t f = 0; f < m->split_jobs[i].n; f += SPLIT_CHUNK) ch.push_back(make_uint2((unsigned)i, (unsigned)f));
+    }
     if (m->split_table) HIPCHK(hipFree(m->split_table));
     m->split_table = nullptr;
-    HIPCHK(hipMalloc(&m->split_table, nj * sizeof(SplitJob)));
+    HIPCHK(hipMalloc(&m->split_table, nj * sizeof(SplitJob) + ch.size() * sizeof(uint2)));
     HIPCHK(hipMemcpy(m->split_table, m->split_jobs.data(), nj * sizeof(SplitJob), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(static_cast<char*>(m->split_table) + nj * sizeof(SplitJob), ch.data(), ch.size() * sizeof(uint2),
+                     hipMemcpyHostToDevice));
     m->split_table_n = nj;
+    m->split_chunks = ch.size();
   }
   const SplitJob* t = static_cast<const SplitJob*>(m->split_table);
+  const uint2* ch = reinterpret_cast<const uint2*>(t + nj);
   absmax_batch_kernel<<<dim3(SPLIT_PARTS, (unsigned)nj), 256, 0, st>>>(t);
   HIPCHK(hipGetLastError());
-  split_batch_kernel<<<dim3(64, (unsigned)nj), 256, 0, st>>>(t);
+  split_batch_kernel<<<(unsigned)m->split_chunks, 256, 0, st>>>(t, ch);
   HIPCHK(hipGetLastError());
 }
 
@@ -564,7 +574,9 @@ static void wgrad(Run& R, const float* dy, const float* x, int N, int H, int W, 
   const int bxy = cdiv(Cout, co_t) * cdiv(K, fast ? 128 : 64);
   // (the x3 kernel runs two 64 KB-LDS blocks per CU: one round of 512 blocks; fewer slabs for
   // wgrad_finish_kernel to read than the fp32 kernel's 1024-block target)
-  int splits = std::max(1, std::min(cdiv(fast ? 512 : 1024, bxy), cdiv(M, 256)));
+  // (the fp32 kernel's small-K / small-Cout layers — the padded input conv, the 1x1 out conv — have
+  // one or two tiles: 64-row splits, so its launch is not a few hundred serial rows per block)
+  int splits = std::max(1, std::min(cdiv(fast ? 512 : 1024, bxy), cdiv(M, fast ? 256 : 64)));
   const int rps = rup(cdiv(M, splits), 16);
   splits = cdiv(M, rps);
   float* part = R.ws.get<float>((size_t)splits * Cout * K);
