@@ -45,10 +45,6 @@
 
 namespace dmx {
 
-#ifndef DMX_WPIPE  // (A/B build) software-pipelined A build, barrier mid-chunk
-#define DMX_WPIPE 1
-#endif
-
 // Diagnostic builds only (-DDMX_DIAG=1, k_wino.hip's dmx_diag_wino_stamps reads them): wave 0 of
 // every block records s_memtime at kernel start, after the prologue barrier, after the chunk loop
 // and at the end, plus the hardware id (XCC, CU), into g_wstamp[launch slot][block] — timing only,
@@ -425,7 +421,7 @@ __global__ __launch_bounds__(512) void wino_kernel(const X3Params P) {
   };
   // (GroupNorm-on-load instances keep the plain loop: their halo store's VALU and registers make the
   // pipelined one spill)
-  if constexpr (DMX_WPIPE && GNA == 0) {
+  if constexpr (GNA == 0) {
   // Software-pipelined A build (one barrier per chunk, in the middle).  Iteration c runs m tile 0's
   // MFMAs beside the build of m tile 1's A fragments (halo buffer c & 1); then, after the barrier
   // that publishes chunk c + 1's halo, m tile 1's MFMAs beside the build of chunk c + 1's m tile 0
