@@ -77,12 +77,13 @@ DMX_DEV float2 gn_stats_from_rowpart(const GnBwdParams& p, int n, double* red) {
   return make_float2((float)mean, (float)(1.0 / sqrt(var + 1e-5)));
 }
 
-DMX_DEV float gn_dy(const GnBwdParams& p, size_t idx, int c, float xh, float& dres_out) {
-  const float y = xh * p.gamma[c] + p.beta[c];
-  const float d = p.dout[idx];
+// dy = dLoss/d(GroupNorm output) from loaded values: dout through the GELU (+ residual) that followed the
+// normalisation in the forward (kernels.h norm_kernel)
+DMX_DEV float gn_dy_v(const GnBwdParams& p, float xh, float g, float bt, float d, float rs, float& dres_out) {
+  const float y = xh * g + bt;
   dres_out = 0.f;
   if (p.res != nullptr) {
-    const float dy = d * gelu_grad(p.res[idx] + y);
+    const float dy = d * gelu_grad(rs + y);
     dres_out = dy;
     return dy;
   }
@@ -91,44 +92,43 @@ DMX_DEV float gn_dy(const GnBwdParams& p, size_t idx, int c, float xh, float& dr
 }
 
 // Pass A, grid (chunks, N): block b of sample n takes pixels [b ppb, (b + 1) ppb).  Thread ->
-// (channels, pixels) ownership: C >= 256: channels tid + 256 q (q < C / 256), every pixel;
-// C < 256 (C | 256): channel tid % C, pixels tid / C + k (256 / C).  Coalesced rows.  Block
-// partials are combined in a fixed order by gn_bwd_apply_kernel.
+// (4 channels, pixels): channels 4 (tid % L4) .. + 3 with L4 = C / 4 (<= 128), pixels tid / L4 + k
+// (256 / L4); float4 loads along coalesced rows.  Block partials are combined in a fixed order by
+// gn_bwd_apply_kernel.
 static __global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const GnBwdParams p) {
   __shared__ double red[8];
-  __shared__ float tg[3][2][256];
+  __shared__ float tg[3][4][256];
   __shared__ double sr[8];
   const int n = blockIdx.y, b = blockIdx.x, tid = threadIdx.x;
   const float2 st = gn_stats_from_rowpart(p, n, red);
-  const bool wide = p.C >= 256;
-  const int cpt = wide ? p.C / 256 : 1, pstep = wide ? 1 : 256 / p.C;
-  const int c0 = wide ? tid : tid % p.C, p0 = wide ? 0 : tid / p.C;
+  const int L4 = p.C / 4, c4 = tid % L4, p0 = tid / L4, pstep = 256 / L4, c = 4 * c4;
   const size_t base = (size_t)n * p.HW * p.C;
   const int pbeg = b * p.ppb, pend = min(p.HW, pbeg + p.ppb);
+  const floatx4 g4 = *reinterpret_cast<const floatx4*>(p.gamma + c), bt4 = *reinterpret_cast<const floatx4*>(p.beta + c);
   float s1 = 0.f, s2 = 0.f;
-  float g1[2] = {0.f, 0.f}, b1[2] = {0.f, 0.f}, e1[2] = {0.f, 0.f};
+  floatx4 g1 = {0.f, 0.f, 0.f, 0.f}, b1 = g1, e1 = g1;
   for (int pix = pbeg + p0; pix < pend; pix += pstep) {
+    const size_t idx = base + (size_t)pix * p.C + c;
+    const floatx4 r4 = *reinterpret_cast<const floatx4*>(p.r + idx), d4 = *reinterpret_cast<const floatx4*>(p.dout + idx);
+    const floatx4 rs4 = p.res != nullptr ? *reinterpret_cast<const floatx4*>(p.res + idx) : floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      if (q >= cpt) break;
-      const int c = c0 + 256 * q;
-      const size_t idx = base + (size_t)pix * p.C + c;
-      const float xh = (p.r[idx] - st.x) * st.y;
+    for (int j = 0; j < 4; ++j) {
+      const float xh = (r4[j] - st.x) * st.y;
       float dres;
-      const float dy = gn_dy(p, idx, c, xh, dres);
-      const float gd = p.gamma[c] * dy;
+      const float dy = gn_dy_v(p, xh, g4[j], bt4[j], d4[j], rs4[j], dres);
+      const float gd = g4[j] * dy;
       s1 += gd;
       s2 += gd * xh;
-      g1[q] += dy * xh;
-      b1[q] += dy;
-      e1[q] += p.dout[idx];
+      g1[j] += dy * xh;
+      b1[j] += dy;
+      e1[j] += d4[j];
     }
   }
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    tg[0][q][tid] = g1[q];
-    tg[1][q][tid] = b1[q];
-    tg[2][q][tid] = e1[q];
+  for (int j = 0; j < 4; ++j) {
+    tg[0][j][tid] = g1[j];
+    tg[1][j][tid] = b1[j];
+    tg[2][j][tid] = e1[j];
   }
   double d1 = s1, d2 = s2;
 #pragma unroll
@@ -146,25 +146,19 @@ static __global__ __launch_bounds__(256) void gn_bwd_reduce_kernel(const GnBwdPa
     p.bsum[2 * blk] = (sr[0] + sr[1]) + (sr[2] + sr[3]);
     p.bsum[2 * blk + 1] = (sr[4] + sr[5]) + (sr[6] + sr[7]);
   }
-  // per-channel sums over the threads sharing a channel, in thread order (deterministic)
-  for (int c = tid; c < p.C; c += 256) {
+  // per-channel sums over the threads sharing a channel group, in thread order (deterministic)
+  for (int cc = tid; cc < p.C; cc += 256) {
+    const int q = cc >> 2, j = cc & 3;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-    if (wide) {
-      const int q = c / 256, t = c % 256;
-      a0 = tg[0][q][t];
-      a1 = tg[1][q][t];
-      a2 = tg[2][q][t];
-    } else {
-      for (int t = c; t < 256; t += p.C) {
-        a0 += tg[0][0][t];
-        a1 += tg[1][0][t];
-        a2 += tg[2][0][t];
-      }
+    for (int t = q; t < 256; t += L4) {
+      a0 += tg[0][j][t];
+      a1 += tg[1][j][t];
+      a2 += tg[2][j][t];
     }
     float* o = p.bch + blk * 3 * p.C;
-    o[c] = a0;
-    o[p.C + c] = a1;
-    o[2 * p.C + c] = a2;
+    o[cc] = a0;
+    o[p.C + cc] = a1;
+    o[2 * p.C + cc] = a2;
   }
 }
 
@@ -211,17 +205,31 @@ static __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const GnBwdPar
   const size_t base = (size_t)n * p.HW * p.C;
   const int per = p.HW * p.C;
   float mx = 0.f;
-  for (int i = blockIdx.x * 256 + tid; i < per; i += gridDim.x * 256) {
-    const int c = i % p.C;
-    const size_t idx = base + i;
-    const float xh = (p.r[idx] - st.x) * st.y;
-    float dres;
-    const float dy = gn_dy(p, idx, c, xh, dres);
-    const float d = st.y * (p.gamma[c] * dy - m1 - xh * m2);
-    p.dr[idx] = d;
-    mx = fmaxf(mx, fabsf(d));
-    if (p.dres_mode == 1) p.dres[idx] = dres;
-    else if (p.dres_mode == 2) p.dres[idx] += dres;
+  for (int i4 = blockIdx.x * 256 + tid; i4 < per / 4; i4 += gridDim.x * 256) {  // float4 along the rows
+    const int c = (4 * i4) % p.C;
+    const size_t idx = base + 4 * (size_t)i4;
+    const floatx4 r4 = *reinterpret_cast<const floatx4*>(p.r + idx), d4 = *reinterpret_cast<const floatx4*>(p.dout + idx);
+    const floatx4 rs4 = p.res != nullptr ? *reinterpret_cast<const floatx4*>(p.res + idx) : floatx4{0.f, 0.f, 0.f, 0.f};
+    const floatx4 g4 = *reinterpret_cast<const floatx4*>(p.gamma + c), bt4 = *reinterpret_cast<const floatx4*>(p.beta + c);
+    floatx4 o4, q4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float xh = (r4[j] - st.x) * st.y;
+      float dres;
+      const float dy = gn_dy_v(p, xh, g4[j], bt4[j], d4[j], rs4[j], dres);
+      o4[j] = st.y * (g4[j] * dy - m1 - xh * m2);
+      q4[j] = dres;
+      mx = fmaxf(mx, fabsf(o4[j]));
+    }
+    *reinterpret_cast<floatx4*>(p.dr + idx) = o4;
+    if (p.dres_mode == 1) {
+      *reinterpret_cast<floatx4*>(p.dres + idx) = q4;
+    } else if (p.dres_mode == 2) {
+      floatx4 a4 = *reinterpret_cast<const floatx4*>(p.dres + idx);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a4[j] += q4[j];
+      *reinterpret_cast<floatx4*>(p.dres + idx) = a4;
+    }
   }
   if (p.amax_part != nullptr) {
     __shared__ float wm[4];

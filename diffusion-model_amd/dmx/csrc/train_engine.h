@@ -636,6 +636,8 @@ static void gn_bwd(Run& R, const float* r, const float2* rp, int nseg, int rrows
                    const float* res, int act, const float* dout, int N, int C, int HW, float* dr, float* dres,
                    int dres_mode, float* ggamma, float* gbeta, float* demb, int demb_stride, int demb_off,
                    int amax_uses = 0) {
+  // (the float4 passes: 4 channels per thread, C / 4 threads per pixel row dividing the 256-thread block)
+  if (C % 4 != 0 || C / 4 > 256 || 256 % (C / 4) != 0) throw Error(DMX_E_INTERNAL, "gn_bwd: C must be 4 x a divisor of 256");
   // pass A over ~512 blocks in total (>= 16 pixels each)
   const int chunks = std::max(1, std::min(cdiv(512, N), cdiv(HW, 16)));
   const int ppb = cdiv(HW, chunks);
