@@ -786,6 +786,8 @@ struct Run {
   // non-null: the next gemm() runs the split-precision implicit GEMM with A scaled on the device by
   // this max|A| slot (training data gradients, train_engine.h dgrad)
   bool fwd_x3 = false;  // training forward: weights with device-split planes (ConvW::inv_dev) run the split GEMM
+  bool colsum_defer = false;               // training backward: final-level column sums batched (train_engine.h)
+  std::vector<ColsumJob> colsums;
   const unsigned* a_amax = nullptr;
   int a_nparts = 0;  // a_amax: that many per-block partial maxima (absmax_part_kernel)
   // train_engine.h dy_amax: the last tensor whose |max| partials were taken

@@ -246,12 +246,11 @@ static __global__ __launch_bounds__(256) void gn_bwd_apply_kernel(const GnBwdPar
 // grid (cdiv(C, 64), row blocks), 4 row groups x 64 columns per block, combined in a fixed order.
 // out_b != nullptr: columns >= cb go to out_b[c - cb] (two adjacent column ranges of one table, e.g. the
 // GroupNorm / LayerNorm gamma and beta gradients, summed by one launch)
-static __global__ __launch_bounds__(256) void colsum_kernel(const float* in, int R, int C, size_t stride, int rpb,
-                                                          float* out, int accumulate, float* out_b = nullptr,
-                                                          int cb = 0) {
+DMX_DEV void colsum_body(const float* in, int R, int C, size_t stride, int rpb, float* out, int accumulate,
+                         float* out_b, int cb, int bx, int by) {
   __shared__ float red[4][64];
-  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6, c = blockIdx.x * 64 + cl;
-  const int r0 = blockIdx.y * rpb, r1 = min(R, r0 + rpb);
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6, c = bx * 64 + cl;
+  const int r0 = by * rpb, r1 = min(R, r0 + rpb);
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;  // 4 independent chains keep loads in flight
   if (c < C) {
     int r = r0 + rg;
@@ -267,9 +266,29 @@ static __global__ __launch_bounds__(256) void colsum_kernel(const float* in, int
   __syncthreads();
   if (rg == 0 && c < C) {
     const float v = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
-    float* o = (out_b != nullptr && c >= cb) ? out_b + (c - cb) : out + (size_t)blockIdx.y * C + c;
+    float* o = (out_b != nullptr && c >= cb) ? out_b + (c - cb) : out + (size_t)by * C + c;
     *o = accumulate ? *o + v : v;
   }
+}
+static __global__ __launch_bounds__(256) void colsum_kernel(const float* in, int R, int C, size_t stride, int rpb,
+                                                          float* out, int accumulate, float* out_b = nullptr,
+                                                          int cb = 0) {
+  colsum_body(in, R, C, stride, rpb, out, accumulate, out_b, cb, blockIdx.x, blockIdx.y);
+}
+// The backward's final-level column sums (parameter gradients nothing in the backward reads again —
+// GroupNorm / LayerNorm gamma and beta, biases), deferred to the end of the pass and run COLSUM_BATCH
+// per launch (blockIdx.y = job; each job one row block, the same per-column order as colsum_kernel)
+constexpr int COLSUM_BATCH = 16;
+struct ColsumJob {
+  const float* in; float* outa; float* outb; size_t stride; int rows, C, cb;
+};
+struct ColsumBatch {
+  ColsumJob j[COLSUM_BATCH];
+};
+static __global__ __launch_bounds__(256) void colsum_batch_kernel(const ColsumBatch b) {
+  const ColsumJob& j = b.j[blockIdx.y];
+  if ((int)blockIdx.x * 64 >= j.C) return;
+  colsum_body(j.in, j.rows, j.C, j.stride, j.rows, j.outa, 0, j.outb, j.cb, blockIdx.x, 0);
 }
 
 // ---------------------------------------------------------------------------

@@ -504,17 +504,43 @@ static void train_fwd_body(Run& R, Tape& T, const TrainArgs& a) {
 // ---------------------------------------------------------------------------
 // out[c] = sum over `rows` rows of in[r * stride + c]: one pass for <= 256 rows, else row
 // blocks of 256 into a partial table, then that table's column sums (fixed order).
+// the final level of a column sum: deferred to colsum_flush (train_bwd_body's end) when R.colsum_defer
+static void colsum_final(Run& R, const float* in, int rows, int C, size_t stride, float* outa, float* outb, int cb) {
+  if (R.colsum_defer) {
+    R.colsums.push_back(ColsumJob{in, outa, outb, stride, rows, C, cb});
+    return;
+  }
+  colsum_kernel<<<dim3(cdiv(C, 64), 1), 256, 0, R.st>>>(in, rows, C, stride, rows, outa, 0, outb, cb);
+  HIPCHK(hipGetLastError());
+}
+
+static void colsum_flush(Run& R) {
+  for (size_t k = 0; k < R.colsums.size(); k += COLSUM_BATCH) {
+    ColsumBatch b;
+    std::memset(&b, 0, sizeof(b));
+    const int nj = (int)std::min<size_t>(COLSUM_BATCH, R.colsums.size() - k);
+    int cmax = 0;
+    for (int i = 0; i < nj; ++i) {
+      b.j[i] = R.colsums[k + i];
+      cmax = std::max(cmax, b.j[i].C);
+    }
+    colsum_batch_kernel<<<dim3(cdiv(cmax, 64), nj), 256, 0, R.st>>>(b);
+    HIPCHK(hipGetLastError());
+  }
+  R.colsums.clear();
+}
+
 static void colsum(Run& R, const float* in, int rows, int C, size_t stride, float* out) {
   const int rpb = 256, nb = cdiv(rows, rpb);
   float* part = nb > 1 ? R.ws.get<float>((size_t)nb * C) : nullptr;
   if (R.plan) return;
   if (nb == 1) {
-    colsum_kernel<<<dim3(cdiv(C, 64), 1), 256, 0, R.st>>>(in, rows, C, stride, rows, out, 0);
+    colsum_final(R, in, rows, C, stride, out, nullptr, 0);
   } else {
     colsum_kernel<<<dim3(cdiv(C, 64), nb), 256, 0, R.st>>>(in, rows, C, stride, rpb, part, 0);
-    colsum_kernel<<<dim3(cdiv(C, 64), 1), 256, 0, R.st>>>(part, nb, C, C, nb, out, 0);
+    HIPCHK(hipGetLastError());
+    colsum_final(R, part, nb, C, C, out, nullptr, 0);
   }
-  HIPCHK(hipGetLastError());
 }
 
 // outa[c] = sum of in[r][c], outb[c] = sum of in[r][C + c] (rows of 2C floats at `stride`): one launch
@@ -524,12 +550,12 @@ static void colsum_pair(Run& R, const float* in, int rows, int C, size_t stride,
   float* part = nb > 1 ? R.ws.get<float>((size_t)nb * 2 * C) : nullptr;
   if (R.plan) return;
   if (nb == 1) {
-    colsum_kernel<<<dim3(cdiv(2 * C, 64), 1), 256, 0, R.st>>>(in, rows, 2 * C, stride, rows, outa, 0, outb, C);
+    colsum_final(R, in, rows, 2 * C, stride, outa, outb, C);
   } else {
     colsum_kernel<<<dim3(cdiv(2 * C, 64), nb), 256, 0, R.st>>>(in, rows, 2 * C, stride, rpb, part, 0);
-    colsum_kernel<<<dim3(cdiv(2 * C, 64), 1), 256, 0, R.st>>>(part, nb, 2 * C, 2 * C, nb, outa, 0, outb, C);
+    HIPCHK(hipGetLastError());
+    colsum_final(R, part, nb, 2 * C, 2 * C, outa, outb, C);
   }
-  HIPCHK(hipGetLastError());
 }
 
 // bias gradient = column sums of dY [M][C]
@@ -826,6 +852,7 @@ static void dense_dx(Run& R, const float* dy, int ldy, const float* w, int rows,
 
 static void train_bwd_body(Run& R, Tape& T, const GradMap& G, const float* d_eps, const float* d_geom) {
   dmx_model* m = R.m;
+  R.colsum_defer = !R.plan;  // the final-level column sums run batched at the end (colsum_flush)
   const int N = T.n, H = T.h, W = T.w, HW = H * W, M = N * HW, Co = m->in_ch;
   // heads
   R.layer = "train.heads.bwd";
@@ -944,6 +971,8 @@ static void train_bwd_body(Run& R, Tape& T, const GradMap& G, const float* d_eps
     for (const char* k : {"cond_mlp.0.weight", "cond_mlp.0.bias", "cond_mlp.2.weight", "cond_mlp.2.bias"})
       zero_grad(R, G, m, k);
   }
+  if (!R.plan) colsum_flush(R);
+  R.colsum_defer = false;
 }
 
 static void check_train(dmx_model* m, int n, int h, int w) {
