@@ -1534,29 +1534,31 @@ static void layernorm(Run& R, const float* x, float* y, const Vec& w, const Vec&
   HIPCHK(hipGetLastError());
 }
 
-// stats (training forward only, exact fp32): the row max / 1 / sum per (sample, head, query) for
-// the backward (train_engine.h attn_core_bwd)
+// stats (training forward only): a softmax reference and 1 / sum per (sample, head, query) for the
+// backward (train_engine.h attn_core_bwd; P = exp(s - ref) / sum holds for any reference)
 static void attention_core(Run& R, const float* qkv, float* out, int N, int L, int C, float* stats = nullptr) {
   if (R.plan) return;
   const int D = C / 4;
   if (D != 16 && D != 32 && D != 64) throw Error(DMX_E_INTERNAL, "attention: unsupported head dim");
-  if (stats != nullptr && R.m->prec != 0) throw Error(DMX_E_INTERNAL, "attention stats: exact-fp32 mode only");
-  if (R.m->prec >= 1 && D == 16 && att16_lds_bytes(L, 0) <= 160 * 1024) {
+  // the split-precision cores: inference in modes 1 / 2, and the training forward (R.fwd_x3, with stats)
+  const bool x3 = R.m->prec >= 1 || (R.fwd_x3 && stats != nullptr);
+  if (stats != nullptr && R.m->prec == 2) throw Error(DMX_E_INTERNAL, "attention stats: not in fp16 mode");
+  if (x3 && D == 16 && att16_lds_bytes(L, 0) <= 160 * 1024) {
     // head resident in LDS (sa5 / sa6): one block per (sample, head), no per-chunk staging
     const int x1 = R.m->prec == 2 ? 1 : 0, nw = L > 256 ? 16 : 8;
     R.begin("attention16_kernel<" + std::to_string(nw) + ", " + std::to_string(x1) + ">", 4.0 * N * (double)L * L * C,
             4.0 * (double)N * L * 4 * C);
-    HIPCHK(launch_attention16(nw, x1, qkv, out, L, C, N, R.st));
+    HIPCHK(launch_attention16(nw, x1, qkv, out, L, C, N, R.st, stats));
     R.end();
     HIPCHK(hipGetLastError());
     return;
   }
-  if (R.m->prec >= 1) {
+  if (x3) {
     dim3 grid(cdiv(L, 128), 4, N);
     const int x1 = R.m->prec == 2 ? 1 : 0, wpe = D == 16 ? 4 : 1;  // D = 16: >= 4 waves / SIMD (register cap)
     R.begin("attention_x3_kernel<" + std::to_string(D) + ", " + std::to_string(wpe) + ", " + std::to_string(x1) + ">",
             4.0 * N * (double)L * L * C, 4.0 * (double)N * L * 4 * C);
-    launch_attention_x3(D, wpe, x1, qkv, out, L, C, grid, R.st);
+    launch_attention_x3(D, wpe, x1, qkv, out, L, C, grid, R.st, stats);
     R.end();
     HIPCHK(hipGetLastError());
     return;

@@ -419,7 +419,7 @@ namespace dmx {
 // X1 = 1: config-4 fp16 arithmetic (Q, K, V, P rounded to f16, one MFMA per product).
 template <int D, int WPE = 1, int X1 = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void attention_x3_kernel(
-    const float* qkv, float* out, int L, int C) {
+    const float* qkv, float* out, int L, int C, float* stats) {
   constexpr int KC = 64, KS = D + 8, VR = D < 32 ? 32 : D, VS = KC + 4, NKS = D / 16, NDT = VR / 32;
   __shared__ __attribute__((aligned(16))) _Float16 Kh[KC][KS];
   __shared__ __attribute__((aligned(16))) _Float16 Kl[X1 ? 1 : KC][KS];
@@ -623,6 +623,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     lrun += __shfl_xor(lrun, 32, 64);
   }
   const float inv = 1.0f / lrun;
+  if (stats != nullptr && fh == 0 && q < L) {  // training forward: (row max, 1 / sum) in natural units
+    float* so = stats + (((size_t)n * 4 + hd) * L + q) * 3;
+    so[0] = mrun * 0.6931471805599453f;
+    so[1] = inv;
+  }
   if (q < L) {
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt)
@@ -678,7 +683,8 @@ DMX_DEV floatx16 mfma_untied(half8 a, half8 b, floatx16 c) {
 }
 
 template <int NW, int X1 = 0>
-__global__ __launch_bounds__(NW * 64) void attention16_kernel(const float* qkv, float* out, int L, int C) {
+__global__ __launch_bounds__(NW * 64) void attention16_kernel(const float* qkv, float* out, int L, int C,
+                                                              float* stats) {
   constexpr int D = 16;
   extern __shared__ __attribute__((aligned(16))) _Float16 att_lds[];
   const int Lp = att16_lp(L), VS = Lp + 4;
@@ -851,6 +857,11 @@ __global__ __launch_bounds__(NW * 64) void attention16_kernel(const float* qkv, 
       }
     }
     const float inv = 1.0f / __shfl(o[8], fr, 64);  // O^T row 16 (the ones row) = the denominator
+    if (stats != nullptr && fh == 0 && q < L) {  // training forward: (reference, 1 / sum) in natural units —
+      float* so = stats + (((size_t)n * 4 + hd) * L + q) * 3;  // P = exp(s - ref) / sum for any reference
+      so[0] = mref * 0.6931471805599453f;
+      so[1] = inv;
+    }
     if (q < L) {
 #pragma unroll
       for (int g = 0; g < 2; ++g) {

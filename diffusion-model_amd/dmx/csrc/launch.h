@@ -45,9 +45,10 @@ void launch_wino_pack(const float* B, int kpad, int cin, int cout, float scale, 
 void launch_f32(int src_mode, int epi, int bm, int bn, const IgemmParams& p, dim3 grid, hipStream_t st);
 // attention cores (k_attn.hip): split-precision (D, waves-per-EU hint, x1) and exact fp32 (D, QT).
 void launch_attention_x3(int D, int wpe, int x1, const float* qkv, float* out, int L, int C, dim3 grid,
-                         hipStream_t st);
+                         hipStream_t st, float* stats = nullptr);
 // D = 16 core with the head resident in LDS; grid (1, 4, N), nw waves per block.
-hipError_t launch_attention16(int nw, int x1, const float* qkv, float* out, int L, int C, int N, hipStream_t st);
+hipError_t launch_attention16(int nw, int x1, const float* qkv, float* out, int L, int C, int N, hipStream_t st,
+                              float* stats = nullptr);
 void launch_attention_f32(int D, int qt, const float* qkv, float* out, int L, int C, dim3 grid, hipStream_t st,
                           float* stats = nullptr);
 // fused attention-block token kernels (tokmlp.h), k_tok.hip.
