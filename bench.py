@@ -305,7 +305,7 @@ def train_leg(args, dev, world=1, rank=0):
            "unit": "training images/s (B=%d per GPU, 224x224 -> 28x28x4 latents)" % B,
            "ms_per_step": round(dt * 1e3, 3), "steps": k, "n_gpus": world,
             "native_forward_ms": round(fwd * 1e3, 3), "native_backward_ms": round((fb - fwd) * 1e3, 3),
-            "dtype": "f32 semantics (GEMMs as x3 split-f16 MFMA products with fp32 accumulation, forward and backward; attention cores fp32 MFMA; fp32 elsewhere)",
+            "dtype": "f32 semantics (GEMMs and the forward attention cores as x3 split-f16 MFMA products with fp32 accumulation; attention backward on fp32 MFMA; fp32 elsewhere)",
             "path": "train_latent_cond.py step on the drop-ins: VAE.encode x4, add_noise, forward, mse + "
                     "masked_geom_mse, loss.backward() (dmx_train_backward), torch Adam"}
     if world > 1:
