@@ -194,3 +194,32 @@ def test_unetcond_training_dropout_draws_like_reference(cuda):
     torch.rand_like(y.float())
     torch.rand(vals.size(0), device=cuda)
     assert torch.equal(after, torch.cuda.get_rng_state(cuda))
+
+
+def test_refreshed_training_weights_equal_fresh_model(cuda):
+    """After optimizer.step() the training weights are re-derived on the device (dmx_model_refresh:
+    the data-gradient packs straight from the forward weights — flipped 3x3 / transposed Linear —
+    the forward and data-gradient f16 planes with their device-side scales): the next forward +
+    backward must equal, bit for bit, that of a model built from scratch from the updated weights."""
+    from models.unet_cond_geom import UnetCondWithGeomHead
+    m, geom = _model("g", cuda)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    loss, _, _ = _loss(m, geom, case_inputs("g"), cuda, 0.5)
+    opt.zero_grad()
+    loss.backward()
+    opt.step()
+    nm0 = m.native()
+    inputs = case_inputs("g", True)
+    loss1, eps1, g1 = _loss(m, geom, inputs, cuda, 0.5)
+    opt.zero_grad()
+    loss1.backward()
+    assert m.native() is nm0  # refreshed, not rebuilt
+    grads1 = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+    fresh = UnetCondWithGeomHead().to(cuda).train()
+    fresh.load_state_dict(m.state_dict())
+    loss2, eps2, g2 = _loss(fresh, geom, inputs, cuda, 0.5)
+    fresh.zero_grad()
+    loss2.backward()
+    assert torch.equal(eps1, eps2) and torch.equal(g1, g2)
+    for n, p in fresh.named_parameters():
+        assert torch.equal(grads1[n], p.grad), n
