@@ -177,8 +177,8 @@ int dmx_vae_encode(dmx_model* m, const float* x, const float* eps, float* z, flo
 
 /* ---- training step (replaces the forward + loss.backward() of UnetCondWithGeomHead / UnetCond
  * in train_latent_cond.py:148-162) ------------------------------------
- * dmx_train_forward: model(x, t, y, cond_vals, cond_mask) in exact fp32 (mode 0 GEMMs whatever
- * the model's precision), recording the activations the backward needs in a tape owned by the
+ * dmx_train_forward: model(x, t, y, cond_vals, cond_mask) with fp32 semantics (x3 split GEMMs with
+ * device-side scales whatever the model's precision), recording the activations the backward needs in a tape owned by the
  * model; x: (n,in_ch,h,w); t, y: (n,) int64 (t in [1, tmax], y in [0, num_classes]);
  * vals/mask: (n,12) or NULL; eps: (n,in_ch,h,w) out; geom: (n,geom_dim) out or NULL.
  * *tape_id identifies the tape (one per model: a later forward replaces it).
